@@ -1,0 +1,101 @@
+// bm_common.h -- shared helpers for libbolt_mi355x (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+#define BM_MAXD 16
+
+// ---------------------------------------------------------------------------
+// FastDiv: 64-bit division by a runtime-invariant divisor with one mul-hi.
+// "Round-up" magic (Hacker's Delight 10-9 / libdivide branchfree u64):
+//   l = ceil(log2 d), m = floor(2^64 (2^l - d) / d) + 1,
+//   q = (t + ((n - t) >> 1)) >> (l - 1),  t = mulhi(m, n)
+// exact for every n < 2^64 and 2 <= d < 2^63; d == 1 is flagged.
+// Host and device share the code so the host test can check it exhaustively.
+// ---------------------------------------------------------------------------
+struct FastDiv {
+  uint64_t d;
+  uint64_t m;
+  uint32_t s;
+  uint32_t is1;
+};
+
+static inline FastDiv make_fastdiv(uint64_t d) {
+  FastDiv f;
+  f.d = d;
+  f.is1 = (d <= 1) ? 1u : 0u;
+  f.m = 0;
+  f.s = 0;
+  if (d <= 1) return f;
+  int l = 64 - __builtin_clzll(d - 1);  // ceil(log2 d), 1..63
+  unsigned __int128 num = ((unsigned __int128)((1ull << l) - d)) << 64;
+  f.m = (uint64_t)(num / d) + 1;
+  f.s = (uint32_t)(l - 1);
+  return f;
+}
+
+__host__ __device__ __forceinline__ uint64_t bm_mulhi(uint64_t a, uint64_t b) {
+  return (uint64_t)(((unsigned __int128)a * (unsigned __int128)b) >> 64);
+}
+
+__host__ __device__ __forceinline__ uint64_t fd_div(uint64_t n, const FastDiv &f) {
+  if (f.is1) return n;
+  uint64_t t = bm_mulhi(f.m, n);
+  return (t + ((n - t) >> 1)) >> f.s;
+}
+
+// Mixed-radix decomposition of a linear index over up to BM_MAXD dims,
+// stored innermost first; accumulates source and destination offsets.
+struct Decomp {
+  int32_t n;
+  int32_t pad_;
+  FastDiv div[BM_MAXD];
+  int64_t ss[BM_MAXD];
+  int64_t ds[BM_MAXD];
+};
+
+__device__ __forceinline__ void decomp2(uint64_t idx, const Decomp &d, int64_t &so,
+                                        int64_t &dof) {
+  so = 0;
+  dof = 0;
+  const int n = d.n;
+  for (int k = 0; k + 1 < n; ++k) {
+    uint64_t q = fd_div(idx, d.div[k]);
+    uint64_t r = idx - q * d.div[k].d;
+    so += (int64_t)r * d.ss[k];
+    dof += (int64_t)r * d.ds[k];
+    idx = q;
+  }
+  if (n > 0) {  // outermost: the remaining index is the coordinate
+    so += (int64_t)idx * d.ss[n - 1];
+    dof += (int64_t)idx * d.ds[n - 1];
+  }
+}
+
+// Byte vectors for wide global accesses.
+template <int NB> struct VecB;
+template <> struct VecB<1> { typedef uint8_t t; };
+template <> struct VecB<2> { typedef uint16_t t; };
+template <> struct VecB<4> { typedef uint32_t t; };
+template <> struct VecB<8> { typedef __attribute__((ext_vector_type(2))) uint32_t t; };
+template <> struct VecB<16> { typedef __attribute__((ext_vector_type(4))) uint32_t t; };
+
+template <typename T, int N>
+__device__ __forceinline__ void vload(const T *p, T (&out)[N]) {
+  typedef typename VecB<N * sizeof(T)>::t V;
+  V v = *reinterpret_cast<const V *>(p);
+  __builtin_memcpy(out, &v, sizeof(V));
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void vstore(T *p, const T (&in)[N]) {
+  typedef typename VecB<N * sizeof(T)>::t V;
+  V v;
+  __builtin_memcpy(&v, in, sizeof(V));
+  *reinterpret_cast<V *>(p) = v;
+}
+
+// thread-local error channel (bm_last_error)
+void bm_set_error(const char *fmt, ...);

@@ -1,0 +1,424 @@
+// bm_copy.hip -- the data-movement kernels of libbolt_mi355x (gfx950).
+//
+// One primitive, bm_copy_strided, serves every record-moving call site of
+// bolt's Spark path (see include/bolt_mi355x.h).  The host side reduces an
+// arbitrary N-d strided copy to a canonical form (unit dims dropped, dims
+// ordered by destination stride, mergeable neighbours fused) and picks one of
+// three kernels:
+//
+//   rowcopy    innermost dim contiguous on both sides (a permutation that
+//              keeps the last axis, chunk pack/unpack of row bands): rows
+//              moved with 16-B vectors, 4 vectors in flight per lane.
+//   transpose  the destination-contiguous dim differs from the source-
+//              contiguous one (swap / .T on the innermost axis): 64x64-element
+//              tiles staged through LDS (row pad of one element breaks the
+//              power-of-two bank stride), 16-B global loads along the source
+//              axis and 16-B stores along the destination axis.
+//   generic    anything else (no unit stride): one element per lane.
+//
+// All three are HBM-bound; algorithmic bytes = 2 * N * elem_bytes.
+#include "bm_common.h"
+#include "../../include/bolt_mi355x.h"
+
+#include <algorithm>
+#include <vector>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;
+constexpr int kTile = 64;
+
+// ---------------------------------------------------------------- rowcopy --
+template <int VB>
+__global__ void __launch_bounds__(kThreads)
+    k_rowcopy(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
+              FastDiv vpr, uint64_t total, int es) {
+  typedef typename VecB<VB>::t V;
+  const uint64_t step = (uint64_t)gridDim.x * kThreads * kUnroll;
+  for (uint64_t base = (uint64_t)blockIdx.x * kThreads * kUnroll + threadIdx.x;
+       base < total; base += step) {
+    V reg[kUnroll];
+    int64_t doff[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t g = base + (uint64_t)u * kThreads;
+      doff[u] = -1;
+      if (g < total) {
+        const uint64_t row = fd_div(g, vpr);
+        const uint64_t v = g - row * vpr.d;
+        int64_t so, dof;
+        decomp2(row, d, so, dof);
+        reg[u] = *reinterpret_cast<const V *>(src + so * es + (int64_t)v * VB);
+        doff[u] = dof * es + (int64_t)v * VB;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (doff[u] >= 0) *reinterpret_cast<V *>(dst + doff[u]) = reg[u];
+    }
+  }
+}
+
+// -------------------------------------------------------------- transpose --
+struct TransDesc {
+  int64_t La;      // extent of the source-contiguous dim a
+  int64_t Lb;      // extent of the destination-contiguous dim b
+  int64_t sb;      // source stride of dim b (elements)
+  int64_t da;      // destination stride of dim a (elements)
+  FastDiv ntA;     // tiles along a
+  FastDiv ntAB;    // tiles per batch element
+  uint64_t ntiles; // total tiles
+  Decomp batch;    // remaining dims
+};
+
+// VA / VB: elements per lane for the global load (along a) / store (along b).
+template <typename T, int VA, int VB>
+__global__ void __launch_bounds__(kThreads)
+    k_transpose(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
+  __shared__ T tile[kTile][kTile + 1];
+  constexpr int NVA = kTile / VA;
+  constexpr int RPA = kThreads / NVA;
+  constexpr int NVB = kTile / VB;
+  constexpr int RPB = kThreads / NVB;
+  const int tx = threadIdx.x % NVA, ty = threadIdx.x / NVA;
+  const int ux = threadIdx.x % NVB, uy = threadIdx.x / NVB;
+  const int ia = tx * VA;
+  const int ib = ux * VB;
+
+  for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
+    const uint64_t bt = fd_div(t, d.ntAB);
+    const uint64_t rem = t - bt * d.ntAB.d;
+    const uint64_t tb = fd_div(rem, d.ntA);
+    const uint64_t ta = rem - tb * d.ntA.d;
+    int64_t so, dof;
+    decomp2(bt, d.batch, so, dof);
+    const int64_t a0 = (int64_t)ta * kTile, b0 = (int64_t)tb * kTile;
+
+    // load: lanes walk dim a (source-contiguous)
+    const T *s = src + so + a0 + b0 * d.sb;
+    const bool fullA = (a0 + ia + VA <= d.La);
+#pragma unroll
+    for (int it = 0; it < kTile / RPA; ++it) {
+      const int rb = ty + it * RPA;
+      if (b0 + rb < d.Lb) {
+        const T *p = s + ia + (int64_t)rb * d.sb;
+        if (fullA) {
+          T v[VA];
+          vload<T, VA>(p, v);
+#pragma unroll
+          for (int k = 0; k < VA; ++k) tile[rb][ia + k] = v[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < VA; ++k)
+            if (a0 + ia + k < d.La) tile[rb][ia + k] = p[k];
+        }
+      }
+    }
+    __syncthreads();
+
+    // store: lanes walk dim b (destination-contiguous)
+    T *q = dst + dof + b0 + a0 * d.da;
+    const bool fullB = (b0 + ib + VB <= d.Lb);
+#pragma unroll
+    for (int it = 0; it < kTile / RPB; ++it) {
+      const int ra = uy + it * RPB;
+      if (a0 + ra < d.La) {
+        T v[VB];
+#pragma unroll
+        for (int k = 0; k < VB; ++k) v[k] = tile[ib + k][ra];
+        T *p = q + (int64_t)ra * d.da + ib;
+        if (fullB) {
+          vstore<T, VB>(p, v);
+        } else {
+#pragma unroll
+          for (int k = 0; k < VB; ++k)
+            if (b0 + ib + k < d.Lb) p[k] = v[k];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- generic --
+template <int ES>
+__global__ void __launch_bounds__(kThreads)
+    k_generic(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
+              uint64_t total) {
+  typedef typename VecB<ES>::t V;
+  const uint64_t step = (uint64_t)gridDim.x * kThreads;
+  for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total; g += step) {
+    int64_t so, dof;
+    decomp2(g, d, so, dof);
+    *reinterpret_cast<V *>(dst + dof * ES) = *reinterpret_cast<const V *>(src + so * ES);
+  }
+}
+
+// ------------------------------------------------------------------- host --
+struct Dim {
+  int64_t n, ss, ds;
+};
+
+bool fill_decomp(Decomp &d, const std::vector<Dim> &outer_to_inner) {
+  const int n = (int)outer_to_inner.size();
+  if (n > BM_MAXD) return false;
+  d.n = n;
+  d.pad_ = 0;
+  for (int k = 0; k < n; ++k) {  // store innermost first
+    const Dim &x = outer_to_inner[n - 1 - k];
+    d.div[k] = make_fastdiv((uint64_t)x.n);
+    d.ss[k] = x.ss;
+    d.ds[k] = x.ds;
+  }
+  for (int k = n; k < BM_MAXD; ++k) {
+    d.div[k] = make_fastdiv(1);
+    d.ss[k] = 0;
+    d.ds[k] = 0;
+  }
+  return true;
+}
+
+int grid_for(uint64_t work_items, uint64_t per_block) {
+  uint64_t g = (work_items + per_block - 1) / per_block;
+  const uint64_t cap = 256ull * 16;  // 256 CUs x 16 resident-ish blocks, then grid-stride
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+bool aligned(const void *p, int64_t a) { return ((uintptr_t)p % (uintptr_t)a) == 0; }
+
+int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int es,
+                   hipStream_t st) {
+  const Dim inner = dims.back();
+  std::vector<Dim> outer(dims.begin(), dims.end() - 1);
+  const int64_t row_bytes = inner.n * es;
+  int VB = 16;
+  for (; VB > 1; VB >>= 1) {
+    if (row_bytes % VB) continue;
+    if (!aligned(src, VB) || !aligned(dst, VB)) continue;
+    bool ok = true;
+    for (const Dim &x : outer)
+      if ((x.ss * es) % VB || (x.ds * es) % VB) ok = false;
+    if (ok) break;
+  }
+  Decomp d;
+  if (!fill_decomp(d, outer)) {
+    bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)outer.size());
+    return BM_E_ARG;
+  }
+  uint64_t rows = 1;
+  for (const Dim &x : outer) rows *= (uint64_t)x.n;
+  const uint64_t vpr = (uint64_t)(row_bytes / VB);
+  const uint64_t total = rows * vpr;
+  const FastDiv fv = make_fastdiv(vpr);
+  const int grid = grid_for(total, (uint64_t)kThreads * kUnroll);
+  switch (VB) {
+    case 16: k_rowcopy<16><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 8: k_rowcopy<8><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 4: k_rowcopy<4><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 2: k_rowcopy<2><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    default: k_rowcopy<1><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+  }
+  return BM_OK;
+}
+
+template <typename T>
+int launch_transpose_t(const T *src, T *dst, const TransDesc &td, int va_vec, int vb_vec,
+                       hipStream_t st) {
+  constexpr int W = 16 / (int)sizeof(T);
+  uint64_t g = td.ntiles;
+  if (g > 0x7fffffffull) g = 0x7fffffffull;
+  const int grid = (int)g;
+  if (va_vec && vb_vec)
+    k_transpose<T, W, W><<<grid, kThreads, 0, st>>>(src, dst, td);
+  else if (va_vec)
+    k_transpose<T, W, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+  else if (vb_vec)
+    k_transpose<T, 1, W><<<grid, kThreads, 0, st>>>(src, dst, td);
+  else
+    k_transpose<T, 1, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+  return BM_OK;
+}
+
+int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, int a, int es,
+                     hipStream_t st) {
+  const int b = (int)dims.size() - 1;
+  std::vector<Dim> batch;
+  for (int k = 0; k < (int)dims.size(); ++k)
+    if (k != a && k != b) batch.push_back(dims[k]);
+  TransDesc td;
+  td.La = dims[a].n;
+  td.Lb = dims[b].n;
+  td.sb = dims[b].ss;
+  td.da = dims[a].ds;
+  if (!fill_decomp(td.batch, batch)) {
+    bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
+    return BM_E_ARG;
+  }
+  const uint64_t ntA = (uint64_t)((td.La + kTile - 1) / kTile);
+  const uint64_t ntB = (uint64_t)((td.Lb + kTile - 1) / kTile);
+  uint64_t nb = 1;
+  for (const Dim &x : batch) nb *= (uint64_t)x.n;
+  td.ntA = make_fastdiv(ntA);
+  td.ntAB = make_fastdiv(ntA * ntB);
+  td.ntiles = ntA * ntB * nb;
+  // 16-B vectors when every source row start (dims other than a) and every
+  // destination row start (dims other than b) is 16-B aligned.
+  bool va = aligned(src, 16), vb = aligned(dst, 16);
+  for (int k = 0; k < (int)dims.size(); ++k) {
+    if (k != a && (dims[k].ss * es) % 16) va = false;
+    if (k != b && (dims[k].ds * es) % 16) vb = false;
+  }
+  switch (es) {
+    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, va, vb, st);
+    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, va, vb, st);
+    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, va, vb, st);
+    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, va, vb, st);
+    default: break;
+  }
+  bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);
+  return BM_E_ARG;
+}
+
+int launch_generic(const char *src, char *dst, const std::vector<Dim> &dims, int es,
+                   hipStream_t st) {
+  Decomp d;
+  if (!fill_decomp(d, dims)) {
+    bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)dims.size());
+    return BM_E_ARG;
+  }
+  uint64_t total = 1;
+  for (const Dim &x : dims) total *= (uint64_t)x.n;
+  const int grid = grid_for(total, kThreads);
+  switch (es) {
+    case 1: k_generic<1><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
+    case 2: k_generic<2><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
+    case 4: k_generic<4><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
+    case 8: k_generic<8><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
+    case 16: k_generic<16><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
+    default:
+      bm_set_error("bm_copy_strided: generic with elem_bytes %d", es);
+      return BM_E_ARG;
+  }
+  return BM_OK;
+}
+
+// Canonical form: unit dims dropped, dims ordered by destination stride
+// (outermost first), mergeable neighbours fused.
+std::vector<Dim> canonicalize(std::vector<Dim> dims) {
+  std::vector<Dim> v;
+  for (const Dim &x : dims)
+    if (x.n != 1) v.push_back(x);
+  std::stable_sort(v.begin(), v.end(), [](const Dim &p, const Dim &q) {
+    if (p.ds != q.ds) return p.ds > q.ds;
+    return p.ss > q.ss;
+  });
+  std::vector<Dim> out;
+  for (const Dim &x : v) {
+    if (!out.empty() && out.back().ss == x.n * x.ss && out.back().ds == x.n * x.ds) {
+      out.back().n *= x.n;
+      out.back().ss = x.ss;
+      out.back().ds = x.ds;
+    } else {
+      out.push_back(x);
+    }
+  }
+  return out;
+}
+
+}  // namespace
+
+extern "C" int bm_copy_strided(const void *src_, void *dst_, int ndim, const int64_t *shape,
+                               const int64_t *src_strides, const int64_t *dst_strides,
+                               int elem_bytes, void *stream) {
+  if (ndim < 0 || ndim > 24 || elem_bytes <= 0 || (ndim > 0 && (!shape || !src_strides || !dst_strides))) {
+    bm_set_error("bm_copy_strided: bad arguments (ndim=%d elem_bytes=%d)", ndim, elem_bytes);
+    return BM_E_ARG;
+  }
+  std::vector<Dim> dims;
+  for (int k = 0; k < ndim; ++k) {
+    if (shape[k] < 0 || src_strides[k] < 0 || dst_strides[k] < 0) {
+      bm_set_error("bm_copy_strided: negative shape/stride at dim %d", k);
+      return BM_E_ARG;
+    }
+    if (shape[k] == 0) return BM_OK;  // empty: nothing to move
+    dims.push_back({shape[k], src_strides[k], dst_strides[k]});
+  }
+  if (!src_ || !dst_) {
+    bm_set_error("bm_copy_strided: null pointer");
+    return BM_E_ARG;
+  }
+  int es = elem_bytes;
+  // Element sizes without a native path move as bytes (extra inner dim).
+  if (es != 1 && es != 2 && es != 4 && es != 8 && es != 16) {
+    for (Dim &x : dims) { x.ss *= es; x.ds *= es; }
+    dims.push_back({es, 1, 1});
+    es = 1;
+  }
+  std::vector<Dim> c = canonicalize(dims);
+  if (c.empty()) c.push_back({1, 1, 1});
+  hipStream_t st = (hipStream_t)stream;
+  const char *src = (const char *)src_;
+  char *dst = (char *)dst_;
+  int rc;
+  const Dim &in = c.back();
+  if (in.ss == 1 && in.ds == 1) {
+    rc = launch_rowcopy(src, dst, c, es, st);
+  } else {
+    int a = -1;
+    if (in.ds == 1 && es <= 8)
+      for (int k = (int)c.size() - 2; k >= 0; --k)
+        if (c[k].ss == 1) { a = k; break; }
+    if (a >= 0) {
+      rc = launch_transpose(src, dst, c, a, es, st);
+    } else if (es == 16 && in.ds == 1) {
+      // 16-B elements that need a transpose: move as pairs of 8-B words
+      for (Dim &x : c) { x.ss *= 2; x.ds *= 2; }
+      c.push_back({2, 1, 1});
+      rc = launch_rowcopy(src, dst, canonicalize(c), 8, st);
+    } else {
+      rc = launch_generic(src, dst, c, es, st);
+    }
+  }
+  if (rc != BM_OK) return rc;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    bm_set_error("bm_copy_strided: launch failed: %s", hipGetErrorString(e));
+    return BM_E_HIP;
+  }
+  return BM_OK;
+}
+
+extern "C" int bm_permute(const void *src, void *dst, int ndim, const int64_t *shape,
+                          const int32_t *perm, int elem_bytes, void *stream) {
+  if (ndim < 0 || ndim > 24 || (ndim > 0 && (!shape || !perm))) {
+    bm_set_error("bm_permute: bad arguments (ndim=%d)", ndim);
+    return BM_E_ARG;
+  }
+  int64_t sstr[24], oshape[24], dstr[24];
+  bool seen[24] = {false};
+  int64_t acc = 1;
+  for (int k = ndim - 1; k >= 0; --k) {
+    sstr[k] = acc;
+    acc *= shape[k];
+  }
+  for (int k = 0; k < ndim; ++k) {
+    const int p = perm[k];
+    if (p < 0 || p >= ndim || seen[p]) {
+      bm_set_error("bm_permute: invalid permutation");
+      return BM_E_ARG;
+    }
+    seen[p] = true;
+    oshape[k] = shape[p];
+  }
+  acc = 1;
+  for (int k = ndim - 1; k >= 0; --k) {
+    dstr[k] = acc;
+    acc *= oshape[k];
+  }
+  int64_t srcs[24];
+  for (int k = 0; k < ndim; ++k) srcs[k] = sstr[perm[k]];
+  return bm_copy_strided(src, dst, ndim, oshape, srcs, dstr, elem_bytes, stream);
+}

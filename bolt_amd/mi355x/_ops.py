@@ -1,0 +1,128 @@
+"""Device operations of the MI355X backend, on byte buffers (torch tensors).
+
+Every array of the backend stores its local shard as a flat ``torch.uint8``
+tensor in HBM; the numpy dtype and shape are host metadata.  The operations
+here launch the libbolt_mi355x kernels on the current HIP stream of the
+tensor's device (torch's stream: hipEvents on it time the kernels).
+
+The backend is chosen per device: HIP for 'cuda' devices.  There is no CPU
+fallback; a non-GPU device raises unless a backend has been registered for
+it explicitly (the multi-process CPU tests register a reference executor to
+check the distributed orchestration -- see tests/cpu_backend.py).
+"""
+import ctypes
+
+import numpy as np
+
+from bolt_amd.mi355x import _lib
+
+_DTYPE_CODES = {
+    np.dtype(np.bool_): _lib.BM_BOOL,
+    np.dtype(np.uint8): _lib.BM_U8,
+    np.dtype(np.int8): _lib.BM_I8,
+    np.dtype(np.uint16): _lib.BM_U16,
+    np.dtype(np.int16): _lib.BM_I16,
+    np.dtype(np.uint32): _lib.BM_U32,
+    np.dtype(np.int32): _lib.BM_I32,
+    np.dtype(np.uint64): _lib.BM_U64,
+    np.dtype(np.int64): _lib.BM_I64,
+    np.dtype(np.float16): _lib.BM_F16,
+    np.dtype(np.float32): _lib.BM_F32,
+    np.dtype(np.float64): _lib.BM_F64,
+}
+
+
+def dtype_code(dtype):
+    dt = np.dtype(dtype)
+    if dt.byteorder == '>':
+        raise NotImplementedError("big-endian dtype %s is not supported on MI355X" % dt)
+    try:
+        return _DTYPE_CODES[dt.newbyteorder('=')]
+    except KeyError:
+        raise NotImplementedError("statistics over dtype %s are not supported by the mi355x mode" % dt)
+
+
+class HipBackend(object):
+    """Launches libbolt_mi355x kernels on torch's current stream."""
+
+    name = "hip"
+
+    def __init__(self):
+        self.lib = _lib.load()
+
+    @staticmethod
+    def _stream(t):
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+    @staticmethod
+    def _ptr(t, off=0):
+        return ctypes.c_void_p(t.data_ptr() + int(off))
+
+    def copy_strided(self, src, src_off, dst, dst_off, shape, sstrides, dstrides, es):
+        """dst[dst_off + idx . dstrides] = src[src_off + idx . sstrides] (offsets in bytes)."""
+        nd = len(shape)
+        if nd == 0:
+            shape, sstrides, dstrides, nd = [1], [1], [1], 1
+        _lib.check(self.lib.bm_copy_strided(self._ptr(src, src_off), self._ptr(dst, dst_off), nd,
+                                            _lib.i64_array(shape), _lib.i64_array(sstrides),
+                                            _lib.i64_array(dstrides), int(es), self._stream(src)),
+                   "bm_copy_strided")
+
+    def permute(self, src, shape, perm, es, dst):
+        _lib.check(self.lib.bm_permute(self._ptr(src), self._ptr(dst), len(shape),
+                                       _lib.i64_array(shape), _lib.i32_array(perm), int(es),
+                                       self._stream(src)), "bm_permute")
+
+    def _workspace(self, stat, code, O, R, I, device):
+        import torch
+        n = ctypes.c_size_t(0)
+        _lib.check(self.lib.bm_reduce_workspace_bytes(stat, code, O, R, I, ctypes.byref(n)),
+                   "bm_reduce_workspace_bytes")
+        if n.value == 0:
+            return None, 0
+        return torch.empty(n.value, dtype=torch.uint8, device=device), n.value
+
+    def reduce(self, stat, src, code, O, R, I, out, out_code):
+        ws, nws = self._workspace(stat, code, O, R, I, src.device)
+        _lib.check(self.lib.bm_reduce(stat, self._ptr(src), code, O, R, I, self._ptr(out), out_code,
+                                      self._ptr(ws) if ws is not None else None, nws,
+                                      self._stream(src)), "bm_reduce")
+
+    def state_bytes(self, stat, code, nout):
+        n = ctypes.c_size_t(0)
+        _lib.check(self.lib.bm_reduce_state_bytes(stat, code, nout, ctypes.byref(n)), "bm_reduce_state_bytes")
+        return n.value
+
+    def reduce_state(self, stat, src, code, O, R, I, state):
+        ws, nws = self._workspace(stat, code, O, R, I, src.device)
+        _lib.check(self.lib.bm_reduce_state(stat, self._ptr(src), code, O, R, I, self._ptr(state),
+                                            self._ptr(ws) if ws is not None else None, nws,
+                                            self._stream(src)), "bm_reduce_state")
+
+    def reduce_combine(self, stat, code, states, counts, nout, out, out_code):
+        _lib.check(self.lib.bm_reduce_combine(stat, code, self._ptr(states), _lib.i64_array(counts),
+                                              len(counts), nout, self._ptr(out), out_code,
+                                              self._stream(states)), "bm_reduce_combine")
+
+
+_BACKENDS = {}
+
+
+def register_backend(device_type, backend):
+    """Install a backend for a torch device type (tests only: 'cpu')."""
+    if backend is None:
+        _BACKENDS.pop(device_type, None)
+    else:
+        _BACKENDS[device_type] = backend
+
+
+def backend_for(device):
+    kind = device.type
+    if kind in _BACKENDS:
+        return _BACKENDS[kind]
+    if kind == "cuda":
+        _BACKENDS["cuda"] = HipBackend()
+        return _BACKENDS["cuda"]
+    raise RuntimeError("bolt_amd: device %s has no backend; the mi355x mode runs on MI355X GPUs "
+                       "(HIP) and has no CPU fallback" % device)

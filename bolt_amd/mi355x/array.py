@@ -1,0 +1,431 @@
+"""BoltArrayMI355X: the 'mi355x' mode array (drop-in for BoltArraySpark's hot path).
+
+Data layout.  The logical array is C-order (keys..., values...) -- one record
+is one contiguous value block, exactly the order of the Spark path's sorted
+records (bolt/spark/array.py:1006-1014).  Each rank holds a slab of the
+leading key axis as a flat uint8 tensor in HBM; shape/split/dtype are host
+metadata (array.py:15-28).
+
+Operations and what replaces the Spark machinery:
+  swap / transpose / T / swapaxes / Keys.transpose / Values.transpose:
+      the net permutation (plan.swap_perm, array.py:716-808) as ONE permute
+      kernel (bm_permute); across GPUs pack -> RCCL all-to-all -> unpack.
+  chunk: ChunkedArrayMI355X (chunk.py), the packed chunk layout in HBM.
+  sum / mean / var / std: one reduction kernel over the aligned layout
+      (array.py:243-395 + statcounter.py), float64 accumulation; across GPUs
+      per-rank states -> all_gather -> ordered Chan combine.
+  toarray / tolocal: D2H (+ all_gather of the slabs).
+"""
+import numpy as np
+
+from bolt_amd.mi355x import _lib
+from bolt_amd.mi355x._ops import backend_for, dtype_code
+from bolt_amd.base import BoltArray
+from bolt_amd.mi355x.context import contiguous_strides, local_shape
+from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, _empty
+from bolt_amd.local import BoltArrayLocal
+from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
+from bolt_amd.utils import tupleize, argpack, inshape, istransposeable
+
+_STAT_CODES = {'mean': _lib.STAT_MEAN, 'variance': _lib.STAT_VAR, 'stdev': _lib.STAT_STD}
+
+
+class BoltArrayMI355X(BoltArray):
+
+    _metadata = {
+        '_shape': None,
+        '_split': None,
+        '_dtype': None,
+        '_ordered': True,
+    }
+
+    def __init__(self, data, shape=None, split=None, dtype=None, ordered=True, context=None,
+                 npartitions=None):
+        self._data = data
+        self._shape = tuple(int(s) for s in shape)
+        self._split = int(split)
+        self._dtype = np.dtype(dtype)
+        self._mode = 'mi355x'
+        self._ordered = ordered
+        self._ctx = context
+        self._npartitions = npartitions
+
+    # ------------------------------------------------------------ creation
+    @property
+    def _constructor(self):
+        return BoltArrayMI355X
+
+    @classmethod
+    def _ingest(cls, arry, permutation, shape, split, dtype, ctx, npartitions):
+        """Host ndarray -> sharded device array (spark/construct.py:43-70).
+
+        Records are ``arry.transpose(permutation)`` in C order while the array
+        keeps ``shape`` -- the reference takes the shape before transposing
+        (construct.py:48 vs :55), so non-leading key axes come back as
+        ``x.transpose(perm).reshape(x.shape)``; this is kept for parity.
+        """
+        import torch
+        dev = ctx.device
+        es = dtype.itemsize
+        arry = np.ascontiguousarray(arry)
+        identity = list(permutation) == list(range(len(shape)))
+        lo, hi = ctx.local_bounds(shape[0])
+        rowbytes = int(np.prod(shape[1:], dtype=np.int64)) * es
+        if identity:
+            host = arry[lo:hi].reshape(-1).view(np.uint8)
+            data = torch.from_numpy(host).to(dev)
+        else:
+            # full array to HBM, permuted on the GPU, then this rank's slab of
+            # the permuted bytes (the reference's reshape to the old shape).
+            full = torch.from_numpy(arry.reshape(-1).view(np.uint8)).to(dev)
+            perm_bytes = _empty(full.numel(), dev)
+            if full.numel():
+                backend_for(dev).permute(full, arry.shape, permutation, es, perm_bytes)
+            data = perm_bytes[lo * rowbytes:hi * rowbytes].clone() if ctx.world_size > 1 else perm_bytes
+        return cls(data, shape=shape, split=split, dtype=dtype, context=ctx, npartitions=npartitions)
+
+    @classmethod
+    def _filled(cls, value, shape, split, dtype, ctx, npartitions):
+        """ones/zeros: one record built on the host, broadcast on the GPU (spark/construct.py:207-222)."""
+        import torch
+        dev = ctx.device
+        es = dtype.itemsize
+        lshape = local_shape(ctx, shape)
+        n = int(np.prod(lshape, dtype=np.int64))
+        data = _empty(n * es, dev)
+        if n:
+            unit = torch.from_numpy(np.full(1, value, dtype=dtype).view(np.uint8).copy()).to(dev)
+            backend_for(dev).copy_strided(unit, 0, data, 0, [n], [0], [1], es)
+        return cls(data, shape=shape, split=split, dtype=dtype, context=ctx, npartitions=npartitions)
+
+    @classmethod
+    def _from_shard(cls, shard, shape, split, dtype, ctx, npartitions):
+        import torch
+        dev = ctx.device
+        if isinstance(shard, np.ndarray):
+            dtype = np.dtype(dtype or shard.dtype)
+            data = torch.from_numpy(np.ascontiguousarray(shard, dtype=dtype).reshape(-1).view(np.uint8)).to(dev)
+        else:
+            if dtype is None:
+                raise ValueError("dtype is required for a device shard")
+            dtype = np.dtype(dtype)
+            t = shard.contiguous()
+            data = t.view(torch.uint8).reshape(-1) if t.dtype != torch.uint8 else t.reshape(-1)
+            if data.device != dev:
+                data = data.to(dev)
+        want = int(np.prod(local_shape(ctx, shape), dtype=np.int64)) * dtype.itemsize
+        if data.numel() != want:
+            raise ValueError("shard holds %d bytes, rank %d of %s needs %d"
+                             % (data.numel(), ctx.rank, str(shape), want))
+        if split < 1 or split > len(shape):
+            raise ValueError("split axis must be in [1, %d], got %d" % (len(shape), split))
+        return cls(data, shape=shape, split=split, dtype=dtype, context=ctx, npartitions=npartitions)
+
+    def _like(self, data, shape, split, dtype=None):
+        return BoltArrayMI355X(data, shape=shape, split=split, dtype=self._dtype if dtype is None else dtype,
+                               context=self._ctx, npartitions=self._npartitions)
+
+    @property
+    def _backend(self):
+        return backend_for(self._data.device)
+
+    @property
+    def _local_shape(self):
+        return local_shape(self._ctx, self._shape)
+
+    # ---------------------------------------------------------- properties
+    @property
+    def shape(self):
+        return self._shape
+
+    @property
+    def size(self):
+        return int(np.prod(self._shape))
+
+    @property
+    def ndim(self):
+        return len(self._shape)
+
+    @property
+    def split(self):
+        return self._split
+
+    @property
+    def dtype(self):
+        return self._dtype
+
+    @property
+    def context(self):
+        return self._ctx
+
+    @property
+    def mask(self):
+        return tuple([1] * self._split + [0] * (self.ndim - self._split))
+
+    @property
+    def keys(self):
+        from bolt_amd.mi355x.shapes import Keys
+        return Keys(self)
+
+    @property
+    def values(self):
+        from bolt_amd.mi355x.shapes import Values
+        return Values(self)
+
+    def cache(self):
+        """No-op: records are resident in HBM (array.py:37-41)."""
+
+    def unpersist(self):
+        """No-op (array.py:43-47)."""
+
+    # ------------------------------------------------------------ movement
+    def _permute(self, perm, split):
+        """x.transpose(perm) as a new array with the given split (one kernel / one all-to-all)."""
+        perm = [int(p) for p in perm]
+        new_shape = tuple(self._shape[p] for p in perm)
+        if perm == list(range(self.ndim)):
+            return self._like(self._data, new_shape, split)
+        data = permute_sharded(self._ctx, self._backend, self._data, self._shape, perm,
+                               self._dtype.itemsize)
+        return self._like(data, new_shape, split)
+
+    def chunk(self, size="150", axis=None, padding=None):
+        """Chunk the values of every record (array.py:678-714) -> ChunkedArrayMI355X."""
+        if type(size) is not str:
+            size = tupleize((size))
+        axis = tupleize((axis))
+        padding = tupleize((padding))
+        from bolt_amd.mi355x.chunk import ChunkedArrayMI355X
+        return ChunkedArrayMI355X._from_array(self, size, axis, padding)
+
+    def swap(self, kaxes, vaxes, size="150"):
+        """Move key axes to the values and value axes to the keys (array.py:716-763).
+
+        Same validation and result as the reference: x.transpose(P) with
+        P = [keys kept] + [moved values] + [moved keys] + [values kept] and
+        split' = split - #kaxes + #vaxes.  ``size`` only chooses the Spark
+        chunking; it is validated the same way (getplan + _chunk checks) and
+        does not change the result.  Executed as one permute kernel.
+        """
+        kaxes = np.asarray(tupleize(kaxes), 'int')
+        vaxes = np.asarray(tupleize(vaxes), 'int')
+        if type(size) is not str:
+            size = tupleize(size)
+
+        if len(kaxes) == self.keys.ndim and len(vaxes) == 0:
+            raise ValueError('Cannot perform a swap that would '
+                             'end up with all data on a single key')
+
+        if len(kaxes) == 0 and len(vaxes) == 0:
+            return self
+
+        # the chunk plan the reference would build (errors surface the same way)
+        vshape = self._shape[self._split:]
+        if not (self._split == self.ndim):
+            plan, pad = getplan(vshape, self._dtype, size, None, None)
+            check_plan(plan, pad, vshape)
+        # axes index boolean masks in the reference (chunk.py:224, :293):
+        # negative axes count from the end, out-of-range ones raise IndexError
+        nv = self.ndim - self._split
+        for k in kaxes:
+            if not -self._split <= k < self._split:
+                raise IndexError("key axis %d out of range for %d keys" % (k, self._split))
+        for v in vaxes:
+            if not -nv <= v < nv:
+                raise IndexError("value axis %d out of range for %d values" % (v, nv))
+        kaxes = [int(k) % self._split for k in kaxes]
+        vaxes = [int(v) % nv for v in vaxes] if nv else []
+
+        perm, newsplit = swap_perm(self.ndim, self._split, kaxes, vaxes)
+        return self._permute(perm, newsplit)
+
+    def transpose(self, *axes):
+        """Permute the axes, split unchanged (array.py:765-808)."""
+        if len(axes) == 0:
+            p = np.arange(self.ndim - 1, -1, -1)
+        else:
+            p = np.asarray(argpack(axes))
+        istransposeable(p, range(self.ndim))
+        return self._permute([int(x) for x in p], self._split)
+
+    @property
+    def T(self):
+        """Reverse the axes (array.py:810-815)."""
+        return self.transpose()
+
+    def swapaxes(self, axis1, axis2):
+        """Interchange two axes (array.py:817-833)."""
+        p = list(range(self.ndim))
+        p[axis1] = axis2
+        p[axis2] = axis1
+        return self.transpose(p)
+
+    # ---------------------------------------------------------- statistics
+    def _reduced(self, axis, stat):
+        """Device reduction of ``axis`` -> host ndarray with the kept axes (ascending).
+
+        Returns (result ndarray, out dtype).  Layout per plan.reduce_layout;
+        if the reduced axes are not one block they are first permuted to the
+        front (what _align's swap does physically, array.py:85-115).
+        """
+        import torch
+        axset = sorted(set(int(a) for a in axis))
+        kept = [i for i in range(self.ndim) if i not in axset]
+        out_shape = tuple(self._shape[i] for i in kept)
+        if stat == _lib.STAT_SUM:
+            out_dtype = self._dtype
+        else:
+            out_dtype = stat_dtype(self._dtype, out_shape)
+        code = dtype_code(self._dtype)
+        ocode = dtype_code(out_dtype)
+        be = self._backend
+        ctx = self._ctx
+        dev = self._data.device
+        es = self._dtype.itemsize
+
+        lshape = self._local_shape
+        src = self._data
+        perm, O, R, I = reduce_layout(lshape, axset)
+        if perm is not None:
+            tmp = _empty(src.numel(), dev)
+            if src.numel():
+                be.permute(src, lshape, perm, es, tmp)
+            src = tmp
+        nloc = int(np.prod(lshape, dtype=np.int64))
+
+        if ctx.world_size == 1 or 0 not in axset:
+            # every output lives on this rank (or this rank's slab of them)
+            loc_out = tuple(lshape[i] for i in kept)
+            nout = int(np.prod(loc_out, dtype=np.int64))
+            out = _empty(nout * out_dtype.itemsize, dev)
+            if nout and nloc:
+                be.reduce(stat, src, code, O, R, I, out, ocode)
+            if ctx.world_size > 1:
+                sizes = []
+                for lo, hi in ctx.bounds(self._shape[0]):
+                    sizes.append(int(np.prod((hi - lo,) + out_shape[1:], dtype=np.int64)) * out_dtype.itemsize)
+                out = all_gather_bytes(ctx, out, sizes)
+            host = out.cpu().numpy().view(out_dtype).reshape(out_shape)
+            return host, out_dtype
+
+        # the sharded axis is reduced: per-rank states, gathered and combined
+        # in rank order (statcounter.py:67-99, deterministic here)
+        nout = int(np.prod(out_shape, dtype=np.int64))
+        sbytes = be.state_bytes(stat, code, nout)
+        state = _empty(sbytes, dev)
+        count = int(np.prod([lshape[i] for i in axset], dtype=np.int64))
+        if count:
+            be.reduce_state(stat, src, code, O, R, I, state)
+        else:
+            state.zero_()
+        counts = []
+        for lo, hi in ctx.bounds(self._shape[0]):
+            c = (hi - lo) * int(np.prod([self._shape[i] for i in axset if i != 0], dtype=np.int64))
+            counts.append(c)
+        states = all_gather_bytes(ctx, state, [sbytes] * ctx.world_size)
+        out = _empty(nout * out_dtype.itemsize, dev)
+        be.reduce_combine(stat, code, states, counts, nout, out, ocode)
+        host = out.cpu().numpy().view(out_dtype).reshape(out_shape)
+        return host, out_dtype
+
+    def _stat(self, axis=None, func=None, name=None, keepdims=False):
+        """Statistic over ``axis`` (array.py:284-334); results are host arrays / scalars."""
+        if axis is None:
+            axis = list(range(len(self.shape)))
+        axis = tupleize(axis)
+
+        if func and not name:
+            return self.reduce(func, axis, keepdims)
+
+        if name and not func:
+            inshape(self.shape, axis)
+            arr, _ = self._reduced(axis, _STAT_CODES[name])
+            if arr.ndim == 0:
+                arr = arr[()]
+            if keepdims:
+                for i in axis:
+                    arr = np.expand_dims(arr, axis=i)
+            return BoltArrayLocal(arr).toscalar()
+
+        raise ValueError('Must specify either a function or a statistic name.')
+
+    def reduce(self, func, axis=(0,), keepdims=False):
+        """Reduce with ``func`` over ``axis`` (array.py:243-282).
+
+        Only elementwise addition (operator.add / numpy.add: the path sum()
+        takes) runs on the GPU; other functions are outside this backend.
+        """
+        import operator
+        if func not in (operator.add, np.add):
+            raise NotImplementedError("the mi355x mode reduces with addition only (sum); got %r" % (func,))
+        axis = tupleize(axis)
+        inshape(self.shape, axis)
+        arr, _ = self._reduced(axis, _lib.STAT_SUM)
+        if arr.ndim == 0:
+            arr = arr[()]
+        if keepdims:
+            for i in axis:
+                arr = np.expand_dims(arr, axis=i)
+        if not isinstance(arr, np.ndarray):
+            return arr
+        elif arr.shape == (1,):
+            return arr[0]
+        return BoltArrayLocal(arr)
+
+    def mean(self, axis=None, keepdims=False):
+        """Mean over ``axis`` (array.py:336-349)."""
+        return self._stat(axis, name='mean', keepdims=keepdims)
+
+    def var(self, axis=None, keepdims=False):
+        """Population variance over ``axis`` (array.py:351-364)."""
+        return self._stat(axis, name='variance', keepdims=keepdims)
+
+    def std(self, axis=None, keepdims=False):
+        """Population standard deviation over ``axis`` (array.py:366-379)."""
+        return self._stat(axis, name='stdev', keepdims=keepdims)
+
+    def sum(self, axis=None, keepdims=False):
+        """Sum over ``axis`` in the input dtype (array.py:381-395; integer sums wrap)."""
+        import operator
+        return self._stat(axis, func=operator.add, keepdims=keepdims)
+
+    # -------------------------------------------------------------- egress
+    def _gathered_bytes(self):
+        ctx = self._ctx
+        if ctx.world_size == 1:
+            return self._data
+        rowbytes = int(np.prod(self._shape[1:], dtype=np.int64)) * self._dtype.itemsize
+        sizes = [(hi - lo) * rowbytes for lo, hi in ctx.bounds(self._shape[0])]
+        return all_gather_bytes(ctx, self._data, sizes)
+
+    def toarray(self):
+        """The whole array on the host (array.py:1006-1014)."""
+        host = self._gathered_bytes().cpu().numpy()
+        return host.view(self._dtype).reshape(self._shape)
+
+    def tolocal(self):
+        """As a local bolt array (array.py:999-1004)."""
+        return BoltArrayLocal(self.toarray())
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.toarray()
+        return a if dtype is None else a.astype(dtype)
+
+    def records(self):
+        """(key tuple, value ndarray) pairs in key order -- the content of
+        ``tordd().sortByKey().collect()`` of the Spark path."""
+        x = self.toarray()
+        kshape = self._shape[:self._split]
+        flat = x.reshape((int(np.prod(kshape, dtype=np.int64)),) + self._shape[self._split:])
+        for i, key in enumerate(np.ndindex(*kshape)):
+            yield tuple(int(k) for k in key), flat[i]
+
+    def tordd(self):
+        from bolt_amd.mi355x.records import RecordView
+        return RecordView(list(self.records()), self._ctx.world_size)
+
+    def __repr__(self):
+        s = "BoltArray\n"
+        s += "mode: %s\n" % self._mode
+        s += "shape: %s\n" % str(self.shape)
+        return s

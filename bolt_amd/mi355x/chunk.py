@@ -1,0 +1,280 @@
+"""ChunkedArrayMI355X: bolt's ChunkedArray (bolt/spark/chunk.py) on MI355X.
+
+A chunked array's records are ``(key + chunk_id, chunk_value)`` pairs
+(chunk.py:87-144).  Here every record's chunks live packed back to back in
+HBM, in chunk-id order, each chunk a dense box of its (padded) extent -- the
+layout described by plan.ChunkGeometry.  Building it (pack) and undoing it
+(unpack, padding removed) are strided-copy kernels, one launch per run of
+equally shaped chunks; records never leave their GPU.
+
+keys_to_values / values_to_keys change which axes are keys and re-chunk the
+moved axes; their result is by construction the chunking of the permuted
+array with the new plan/padding (chunk.py:202-347), so they run as
+unpack -> permute (RCCL all-to-all if the sharded axis moves) -> pack.
+"""
+import numpy as np
+
+from bolt_amd.mi355x.context import local_shape
+from bolt_amd.mi355x.dist import permute_sharded, _empty
+from bolt_amd.mi355x.plan import (ChunkGeometry, getplan, check_plan, getnumber, getslices, getmask,
+                           removepad_slices)
+
+
+class ChunkedArrayMI355X(object):
+
+    _metadata = ['_shape', '_split', '_dtype', '_plan', '_padding', '_ordered']
+
+    def __init__(self, packed, shape=None, split=None, dtype=None, plan=None, padding=None,
+                 ordered=True, context=None):
+        self._packed = packed
+        self._shape = tuple(int(s) for s in shape)
+        self._split = int(split)
+        self._dtype = np.dtype(dtype)
+        self._plan = np.asarray(plan, dtype=int)
+        self._padding = np.asarray(padding, dtype=int)
+        self._ordered = ordered
+        self._ctx = context
+        self._geom = ChunkGeometry(self.vshape, self._plan, self._padding)
+
+    # ---------------------------------------------------------- properties
+    @property
+    def dtype(self):
+        return self._dtype
+
+    @property
+    def shape(self):
+        return self._shape
+
+    @property
+    def split(self):
+        return self._split
+
+    @property
+    def plan(self):
+        return self._plan
+
+    @property
+    def padding(self):
+        return self._padding
+
+    @property
+    def uniform(self):
+        """Every value axis divides evenly by its chunk size (chunk.py:54-56)."""
+        return all([np.mod(x, y) == 0 for x, y in zip(self.vshape, self.plan)])
+
+    @property
+    def padded(self):
+        return not all([p == 0 for p in self.padding])
+
+    @property
+    def kshape(self):
+        return np.asarray(self._shape[:self._split])
+
+    @property
+    def vshape(self):
+        return np.asarray(self._shape[self._split:])
+
+    def kmask(self, axes):
+        return self.getmask(axes, len(self.kshape))
+
+    def vmask(self, axes):
+        return self.getmask(axes, len(self.vshape))
+
+    @property
+    def _constructor(self):
+        return ChunkedArrayMI355X
+
+    # host helpers with the reference's names (chunk.py:434-636)
+    def getplan(self, size="150", axes=None, padding=None):
+        return getplan(self.vshape, self._dtype, size, axes, padding)
+
+    @staticmethod
+    def removepad(idx, value, number, padding, axes=None):
+        return value[removepad_slices(idx, number, padding, axes)]
+
+    @staticmethod
+    def getnumber(plan, shape):
+        return getnumber(plan, shape)
+
+    @staticmethod
+    def getslices(plan, padding, shape):
+        return getslices(plan, padding, shape)
+
+    @staticmethod
+    def getmask(inds, n):
+        return getmask(inds, n)
+
+    # --------------------------------------------------------- pack/unpack
+    @staticmethod
+    def _pack(ctx, backend, dense, shape, split, dtype, plan, padding):
+        """Packed chunk buffer for this rank's records of a dense sharded array."""
+        es = np.dtype(dtype).itemsize
+        lshape = local_shape(ctx, shape)
+        nrec = int(np.prod(lshape[:split], dtype=np.int64))
+        vshape = shape[split:]
+        geom = ChunkGeometry(vshape, plan, padding)
+        rec = int(np.prod(vshape, dtype=np.int64))
+        packed = _empty(nrec * geom.size * es, dense.device)
+        if nrec:
+            for (cshape, dstr, pstr, doff, poff) in geom.copies(unpack=False):
+                backend.copy_strided(dense, doff * es, packed, poff * es, [nrec] + cshape,
+                                     [rec] + dstr, [geom.size] + pstr, es)
+        return packed
+
+    def _unpack(self):
+        """Dense bytes of this rank's records (padding removed, chunk.py:146-200)."""
+        es = self._dtype.itemsize
+        lshape = local_shape(self._ctx, self._shape)
+        nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
+        rec = int(np.prod(self.vshape, dtype=np.int64))
+        dense = _empty(nrec * rec * es, self._packed.device)
+        if nrec:
+            be = self._backend
+            for (cshape, dstr, pstr, doff, poff) in self._geom.copies(unpack=True):
+                be.copy_strided(self._packed, poff * es, dense, doff * es, [nrec] + cshape,
+                                [self._geom.size] + pstr, [rec] + dstr, es)
+        return dense
+
+    @property
+    def _backend(self):
+        from bolt_amd.mi355x._ops import backend_for
+        return backend_for(self._packed.device)
+
+    @classmethod
+    def _from_array(cls, barray, size="150", axis=None, padding=None):
+        """ChunkedArray._chunk (chunk.py:87-144) on a BoltArrayMI355X."""
+        shape, split, dtype = barray.shape, barray.split, barray.dtype
+        if split == len(shape) and padding is None:
+            # all keys: every record gets a trailing value axis of length 1
+            shape = shape + (1,)
+            plan, pad = np.array([1]), np.array([0])
+        else:
+            vshape = shape[split:]
+            plan, pad = getplan(vshape, dtype, size, axis, padding)
+            check_plan(plan, pad, vshape)
+        packed = cls._pack(barray._ctx, barray._backend, barray._data, shape, split, dtype, plan, pad)
+        return cls(packed, shape=shape, split=split, dtype=dtype, plan=plan, padding=pad,
+                   ordered=barray._ordered, context=barray._ctx)
+
+    def _rechunk(self, dense, perm, shape_before, newshape, newsplit, newplan, newpadding):
+        """Permute this rank's dense records (exchange if the sharded axis moves) and pack."""
+        es = self._dtype.itemsize
+        if list(perm) != list(range(len(perm))):
+            dense = permute_sharded(self._ctx, self._backend, dense, shape_before, perm, es)
+        packed = self._pack(self._ctx, self._backend, dense, newshape, newsplit, self._dtype,
+                            newplan, newpadding)
+        return self._constructor(packed, shape=newshape, split=newsplit, dtype=self._dtype,
+                                 plan=newplan, padding=newpadding, ordered=True, context=self._ctx)
+
+    # ------------------------------------------------------------- the API
+    def unchunk(self):
+        """Back to a BoltArrayMI355X (chunk.py:146-200); a trailing (1,) value axis is squeezed."""
+        from bolt_amd.mi355x.array import BoltArrayMI355X
+        dense = self._unpack()
+        if np.array_equal(self.vshape, [1]):
+            newshape = self.shape[:-1]
+        else:
+            newshape = self.shape
+        return BoltArrayMI355X(dense, shape=newshape, split=self._split, dtype=self._dtype,
+                               context=self._ctx)
+
+    def keys_to_values(self, axes, size=None):
+        """Move key axes to the front of the values, chunked by ``size`` (chunk.py:202-289)."""
+        if len(axes) == 0:
+            return self
+        kmask = self.kmask(axes)
+        if size is None:
+            size = self.kshape[kmask]
+        newplan = np.r_[size, self.plan].astype(int)
+        newsplit = self._split - len(axes)
+        newshape = tuple(np.r_[self.kshape[~kmask], self.kshape[kmask], self.vshape].astype(int).tolist())
+        newpadding = np.r_[np.zeros(len(axes), dtype=int), self.padding].astype(int)
+        ks = np.arange(self._split)
+        perm = list(ks[~kmask]) + list(ks[kmask]) + list(range(self._split, len(self._shape)))
+        dense = self._unpack()
+        if np.array_equal(self.vshape, [1]):
+            # the singleton value axis of an all-keys chunking is squeezed
+            # (chunk.py:284-287; padding and stale chunk id trimmed as numpy<1.13 did)
+            newshape = newshape[:-1]
+            newplan = newplan[:-1]
+            newpadding = newpadding[:len(newplan)]
+            return self._rechunk(dense, perm[:-1], self._shape[:-1], newshape, newsplit,
+                                 newplan, newpadding)
+        return self._rechunk(dense, perm, self._shape, newshape, newsplit, newplan, newpadding)
+
+    def values_to_keys(self, axes):
+        """Move value axes to the end of the keys (chunk.py:291-347)."""
+        vmask = self.vmask(axes)
+        newplan = self.plan[~vmask]
+        newsplit = self._split + len(axes)
+        newshape = tuple(np.r_[self.kshape, self.vshape[vmask], self.vshape[~vmask]].astype(int).tolist())
+        newpadding = self.padding[~vmask]
+        vs = np.arange(len(self.vshape))
+        perm = (list(range(self._split)) + [self._split + v for v in vs[vmask]] +
+                [self._split + v for v in vs[~vmask]])
+        dense = self._unpack()
+        shape_before = self._shape
+        if len(newshape) == newsplit:
+            newshape = newshape + (1,)
+            newplan = np.array([1])
+            newpadding = np.array([0])
+            perm = perm + [len(perm)]
+            shape_before = shape_before + (1,)
+        return self._rechunk(dense, perm, shape_before, newshape, newsplit, newplan, newpadding)
+
+    # ------------------------------------------------------------- records
+    def records(self):
+        """((key..., chunk id...), chunk ndarray) in key order (``tordd().sortByKey()``)."""
+        from bolt_amd.mi355x.dist import all_gather_bytes
+        ctx = self._ctx
+        es = self._dtype.itemsize
+        g = self._geom
+        if ctx.world_size > 1:
+            per = g.size * int(np.prod(self._shape[1:self._split], dtype=np.int64)) * es
+            sizes = [(hi - lo) * per for lo, hi in ctx.bounds(self._shape[0])]
+            buf = all_gather_bytes(ctx, self._packed, sizes)
+        else:
+            buf = self._packed
+        host = buf.cpu().numpy().view(self._dtype)
+        kshape = self._shape[:self._split]
+        ids = g.chunk_ids()
+        for i, key in enumerate(np.ndindex(*kshape)):
+            base = i * g.size
+            for j in ids:
+                off = g.chunk_offset(j)
+                cs = g.chunk_shape(j)
+                n = int(np.prod(cs, dtype=np.int64))
+                yield (tuple(int(k) for k in key) + tuple(int(c) for c in j),
+                       host[base + off: base + off + n].reshape(cs).copy())
+
+    def tordd(self):
+        from bolt_amd.mi355x.records import RecordView
+        return RecordView(list(self.records()), self._ctx.world_size)
+
+    @property
+    def _rdd(self):
+        return self.tordd()
+
+    def cache(self):
+        """No-op: resident in HBM (chunk.py:648-652)."""
+
+    def unpersist(self):
+        """No-op (chunk.py:654-658)."""
+
+    def __str__(self):
+        s = "Chunked BoltArray\n"
+        s += "shape: %s\n" % str(self.shape)
+        return s
+
+    def __repr__(self):
+        string = str(self)
+        if np.array_equal(self.vshape, [1]):
+            newlines = [i for (i, char) in enumerate(string) if char == '\n']
+            string = string[:newlines[-2] + 1]
+            string += "shape: %s\n" % str(self.shape[:-1])
+        string += "chunk size: %s\n" % str(tuple(self.plan))
+        if self.padded:
+            string += "padding: %s\n" % str(tuple(self.padding))
+        else:
+            string += "padding: none\n"
+        return string

@@ -1,0 +1,360 @@
+"""Host-side planning for the MI355X backend: chunk plans, chunk geometry,
+net permutations of swap/transpose, reduction layouts and result dtypes.
+
+Everything here is integer/shape arithmetic that decides what the HIP kernels
+do; no data is touched.  Each function restates (not copies) the reference
+semantics it cites, including the quirks a drop-in must keep.
+"""
+from itertools import product
+
+import numpy as np
+
+
+# --------------------------------------------------------------------------
+# chunk plans  (bolt/spark/chunk.py)
+# --------------------------------------------------------------------------
+
+def getmask(inds, n):
+    """Boolean mask of length n with ``inds`` set (chunk.py:620-636)."""
+    inds = np.asarray(inds, 'int')
+    mask = np.zeros(n, dtype=bool)
+    mask[inds] = True
+    return mask
+
+
+def getplan(vshape, dtype, size="150", axes=None, padding=None):
+    """Chunk plan (elements per chunk along each value axis) and padding.
+
+    Restates ChunkedArray.getplan (chunk.py:434-512):
+      * str size = kilobytes x 1000 bytes (chunk.py:483); greedy over the value
+        axes in order: an axis whose full extent keeps the chunk >= size gets
+        chunk 1, the first axis that does not gets floor(size/minsize) (capped
+        at its extent) and every later axis stays whole (chunk.py:494-505);
+        size <= itemsize gives all ones (chunk.py:490-491);
+      * tuple size is written onto ``axes`` (chunk.py:478-479);
+      * padding (int or tuple) is broadcast onto ``axes`` (chunk.py:473-475);
+      * anything else -> ValueError (chunk.py:509-510).
+    ``vshape`` is the value shape, ``dtype`` the array dtype.
+    """
+    vshape = np.asarray(vshape)
+    plan = vshape.copy()
+
+    if axes is None:
+        if isinstance(size, str):
+            axes = np.arange(len(vshape))
+        else:
+            axes = np.arange(len(size))
+    else:
+        axes = np.asarray(axes, 'int')
+
+    pad = np.array(len(vshape) * [0, ])
+    if padding is not None:
+        pad[axes] = padding
+
+    if isinstance(size, tuple):
+        plan[axes] = size
+    elif isinstance(size, str):
+        size = 1000.0 * float(size)
+        elsize = np.dtype(dtype).itemsize
+        nelements = np.prod(vshape)
+        dims = vshape[getmask(axes, len(vshape))]
+        if size <= elsize:
+            s = np.ones(len(axes))
+        else:
+            remsize = 1.0 * nelements * elsize
+            s = []
+            for (i, d) in enumerate(dims):
+                minsize = remsize / d
+                if minsize >= size:
+                    s.append(1)
+                    remsize = minsize
+                    continue
+                else:
+                    s.append(min(d, np.floor(size / minsize)))
+                    s[i + 1:] = plan[i + 1:]
+                    break
+        plan[axes] = s
+    else:
+        raise ValueError("Chunk size not understood, must be tuple or int")
+
+    return plan, pad
+
+
+def check_plan(plan, padding, vshape):
+    """The two validations of ChunkedArray._chunk (chunk.py:123-129)."""
+    if any([x + y > z for x, y, z in zip(plan, padding, vshape)]):
+        raise ValueError("Chunk sizes %s plus padding sizes %s cannot exceed value dimensions %s along any axis"
+                         % (tuple(plan), tuple(padding), tuple(vshape)))
+    if any([x > y for x, y in zip(padding, plan)]):
+        raise ValueError("Padding sizes %s cannot exceed chunk sizes %s along any axis"
+                         % (tuple(padding), tuple(plan)))
+
+
+def getnumber(plan, shape):
+    """Chunks per axis, ceil(d / size) (chunk.py:552-572)."""
+    return [int(np.ceil(1.0 * d / size)) for size, d in zip(plan, shape)]
+
+
+def getslices(plan, padding, shape):
+    """Per-axis chunk slices (chunk.py:574-618).
+
+    Chunk j < floor(d/s) spans [j*s - (j>0)*p, j*s + s + p) (the right pad is
+    always added -- ``idx == nchunks`` at chunk.py:609 never holds -- and numpy
+    clips it at d); a remainder chunk spans [floor(d/s)*s - p, d).
+    """
+    slices = []
+    for size, pad, d in zip(plan, padding, shape):
+        size, pad, d = int(size), int(pad), int(d)
+        nchunks = d // size
+        remainder = d % size
+        start = 0
+        end = 0
+        dimslices = []
+        for idx in range(nchunks):
+            end = start + size
+            left = start if idx == 0 else start - pad
+            right = end + pad
+            dimslices.append(slice(left, right, 1))
+            start = end
+        if remainder:
+            dimslices.append(slice(end - pad, d, 1))
+        slices.append(dimslices)
+    return slices
+
+
+def removepad_slices(idx, number, padding, axes=None):
+    """Slices that strip padding from chunk ``idx`` (chunk.py:514-550).
+
+    Left pad is removed unless the chunk is first, right pad unless last, only
+    on ``axes`` with non-zero padding.  Returned as a tuple (the reference
+    indexes with a list, which numpy >= 1.23 rejects).
+    """
+    if axes is None:
+        axes = range(len(number))
+    mask = len(number) * [False, ]
+    for i in range(len(mask)):
+        if i in axes and padding[i] != 0:
+            mask[i] = True
+    starts = [0 if (i == 0 or not m) else p for (i, m, p) in zip(idx, mask, padding)]
+    stops = [None if (i == n - 1 or not m) else -p for (i, m, p, n) in zip(idx, mask, padding, number)]
+    return tuple(slice(i1, i2) for (i1, i2) in zip(starts, stops))
+
+
+# --------------------------------------------------------------------------
+# chunk geometry -> strided copies for the pack / unpack kernels
+# --------------------------------------------------------------------------
+
+def axis_chunks(d, s, p):
+    """Per-chunk (start, extent, core_offset, core_extent) along one axis.
+
+    start/extent: the padded slice of getslices clipped to [0, d);
+    core: the part removepad keeps (the chunk's own cells, chunk.py:546-550):
+    [j*s, min(d, (j+1)*s)), at offset j*s - start inside the chunk.
+    """
+    out = []
+    for j, slc in enumerate(getslices([s], [p], [d])[0]):
+        start = max(0, slc.start)
+        stop = min(d, slc.stop)
+        core_lo = j * s
+        core_hi = min(d, (j + 1) * s)
+        out.append((start, stop - start, core_lo - start, core_hi - core_lo))
+    return out
+
+
+def _runs(chunks, s):
+    """Group consecutive chunks into runs with equal extents and start step s.
+
+    Returns a list of (j0, count, start0, extent, core_off, core_ext) whose
+    members are chunks j0..j0+count-1 with start = start0 + (j-j0)*s.
+    """
+    runs = []
+    for j, (st, ex, co, ce) in enumerate(chunks):
+        if runs:
+            j0, cnt, st0, ex0, co0, ce0 = runs[-1]
+            if (ex, co, ce) == (ex0, co0, ce0) and st == st0 + cnt * s:
+                runs[-1] = (j0, cnt + 1, st0, ex0, co0, ce0)
+                continue
+        runs.append((j, 1, st, ex, co, ce))
+    return runs
+
+
+class ChunkGeometry(object):
+    """Packed layout of one record's chunks for a value shape, plan and padding.
+
+    A record's chunks are stored back to back in C order of their chunk ids
+    (the order of ``product(*slices)`` at chunk.py:132, which is also the
+    sortByKey order of the chunk records); each chunk is a dense C-order box
+    of its padded extent.  With E_a = sum_j extent_a[j], the record holds
+    S = prod_a E_a elements and chunk j starts at
+        off(j) = sum_a P_a[j_a] * prod_{b<a} extent_b[j_b] * prod_{b>a} E_b
+    where P_a is the prefix sum of extents along axis a.
+    """
+
+    def __init__(self, vshape, plan, padding):
+        self.vshape = tuple(int(x) for x in vshape)
+        self.plan = tuple(int(x) for x in plan)
+        self.padding = tuple(int(x) for x in padding)
+        n = len(self.vshape)
+        self.chunks = [axis_chunks(self.vshape[a], self.plan[a], self.padding[a]) for a in range(n)]
+        self.nchunks = tuple(len(c) for c in self.chunks)
+        self.E = [sum(c[1] for c in ch) for ch in self.chunks]
+        self.P = []
+        for ch in self.chunks:
+            pre, acc = [], 0
+            for c in ch:
+                pre.append(acc)
+                acc += c[1]
+            self.P.append(pre)
+        self.size = int(np.prod(self.E)) if n else 1
+        self.runs = [_runs(self.chunks[a], self.plan[a]) for a in range(n)]
+
+    def chunk_offset(self, j):
+        n = len(self.vshape)
+        off = 0
+        for a in range(n):
+            term = self.P[a][j[a]]
+            for b in range(a):
+                term *= self.chunks[b][j[b]][1]
+            for b in range(a + 1, n):
+                term *= self.E[b]
+            off += term
+        return off
+
+    def chunk_shape(self, j):
+        return tuple(self.chunks[a][j[a]][1] for a in range(len(self.vshape)))
+
+    def chunk_ids(self):
+        return list(product(*[range(k) for k in self.nchunks]))
+
+    def copies(self, unpack=False):
+        """Strided copies (per record) between the dense record and the packed record.
+
+        Each entry: (shape, dense_strides, packed_strides, dense_offset,
+        packed_offset) in elements over the index space
+        [count_0..count_{n-1}, extent_0..extent_{n-1}] of one run combination.
+        pack copies padded boxes; unpack copies the cores (padding removed).
+        """
+        n = len(self.vshape)
+        vstride = [1] * n
+        for a in range(n - 2, -1, -1):
+            vstride[a] = vstride[a + 1] * self.vshape[a + 1]
+        out = []
+        for combo in product(*self.runs):
+            shape, dstr, pstr = [], [], []
+            doff, poff = 0, 0
+            ext = [r[3] for r in combo]
+            for a, (j0, cnt, st0, ex, co, ce) in enumerate(combo):
+                # packed stride of chunk index along a, and base offset
+                mult = 1
+                for b in range(a):
+                    mult *= ext[b]
+                for b in range(a + 1, n):
+                    mult *= self.E[b]
+                poff += self.P[a][j0] * mult
+                shape.append(cnt)
+                dstr.append(self.plan[a] * vstride[a])
+                pstr.append(ex * mult)
+                doff += (st0 + (co if unpack else 0)) * vstride[a]
+            inner = [1] * n
+            for a in range(n - 2, -1, -1):
+                inner[a] = inner[a + 1] * ext[a + 1]
+            for a, (j0, cnt, st0, ex, co, ce) in enumerate(combo):
+                shape.append(ce if unpack else ex)
+                dstr.append(vstride[a])
+                pstr.append(inner[a])
+                if unpack:
+                    poff += co * inner[a]
+            out.append((shape, dstr, pstr, doff, poff))
+        return out
+
+
+# --------------------------------------------------------------------------
+# swap / transpose  (bolt/spark/array.py)
+# --------------------------------------------------------------------------
+
+def swap_perm(ndim, split, kaxes, vaxes):
+    """Net permutation and split of BoltArraySpark.swap (array.py:716-763).
+
+    chunk -> keys_to_values(K) -> values_to_keys(V) -> unchunk moves the key
+    axes K (as a set: boolean masks, chunk.py:224/:293) to the front of the
+    values and the value axes V to the end of the keys:
+        P = [k not in K] + [split+v, v in V] + [k in K] + [split+v, v not in V]
+        split' = split - #K + #V.
+    """
+    K = sorted(set(int(k) for k in kaxes))
+    V = sorted(set(int(v) for v in vaxes))
+    keys = list(range(split))
+    vals = list(range(ndim - split))
+    perm = ([k for k in keys if k not in K] + [split + v for v in V] + K +
+            [split + v for v in vals if v not in V])
+    return perm, split - len(K) + len(V)
+
+
+def transpose_split(p, split):
+    """Decomposition of BoltArraySpark.transpose (array.py:788-806).
+
+    Returns (swapping_keys, swapping_values relative to the values); the net
+    result is x.transpose(p) with the split unchanged.
+    """
+    p = np.asarray(p)
+    new_keys, new_values = p[:split], p[split:]
+    swapping_keys = np.sort(new_values[new_values < split])
+    swapping_values = np.sort(new_keys[new_keys >= split])
+    return swapping_keys, swapping_values - split
+
+
+# --------------------------------------------------------------------------
+# reductions  (bolt/spark/array.py:_align, _stat, reduce)
+# --------------------------------------------------------------------------
+
+def reduce_layout(shape, axes):
+    """Kernel layout for reducing ``axes`` of a C-contiguous array.
+
+    Returns (perm, O, R, I): if ``perm`` is None the array is read in place
+    as [O][R][I] (the reduced axes form one contiguous block once unit axes
+    are ignored); otherwise it must first be permuted by ``perm`` (reduced
+    axes first) and is then [1][R][I].  Outputs come out with the kept axes
+    in ascending order, which is what _align's swap produces (array.py:85-115:
+    reduced axes become the keys, kept axes the values in their order).
+    """
+    shape = tuple(int(x) for x in shape)
+    red = set(int(a) for a in axes)
+    labels = []
+    for i, n in enumerate(shape):
+        if n == 1:
+            continue
+        lab = 'R' if i in red else 'K'
+        if labels and labels[-1][0] == lab:
+            labels[-1][1] *= n
+        else:
+            labels.append([lab, n])
+    nR = sum(1 for l in labels if l[0] == 'R')
+    if nR == 0:
+        O = int(np.prod([l[1] for l in labels])) if labels else 1
+        return None, O, 1, 1
+    if nR == 1:
+        pos = [i for i, l in enumerate(labels) if l[0] == 'R'][0]
+        O = int(np.prod([l[1] for l in labels[:pos]])) if pos else 1
+        R = labels[pos][1]
+        I = int(np.prod([l[1] for l in labels[pos + 1:]])) if pos + 1 < len(labels) else 1
+        return None, O, R, I
+    perm = [i for i in range(len(shape)) if i in red] + [i for i in range(len(shape)) if i not in red]
+    R = int(np.prod([shape[i] for i in range(len(shape)) if i in red]))
+    I = int(np.prod([shape[i] for i in range(len(shape)) if i not in red]))
+    return perm, 1, R, I
+
+
+def stat_dtype(dtype, rec_shape):
+    """Result dtype of a StatCounter statistic (statcounter.py:51-59).
+
+    The counter starts at mu = 0.0 (a Python float) and every statistic is
+    built from ``value - mu``, so the result dtype is that of
+    ``record - 0.0`` under the host numpy: float32 stays float32, integers
+    and bool become float64; a 0-d record follows the host numpy's scalar
+    casting rules.  Evaluated, not tabulated, so it matches the reference
+    under whatever numpy is installed.
+    """
+    rec = np.zeros(tuple(rec_shape), dtype=dtype)
+    if len(rec_shape) == 0:
+        rec = rec[()]
+    return np.asarray(rec - 0.0).dtype

@@ -1,0 +1,441 @@
+"""CPU oracle: a record-level numpy restatement of bolt's Spark-mode hot path.
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker -- never by bolt_amd (the product
+path has no CPU fallback).
+
+It restates, record by record and partition by partition, what the reference
+does with an RDD of (key tuple, value ndarray) records (beautifulNow1992/bolt
+v0.7.1; file:line per function).  A "partitioned record set" is a list of
+partitions, each a list of (key, value) pairs, as Spark local[N] holds them.
+Pinned against fixtures produced by the reference itself
+(tests/golden/make_golden.py -> tests/golden/golden.{json,npz});
+tests/test_oracle_golden.py checks every fixture.
+
+Numerics follow the reference: StatCounter's Welford merge runs in the record
+dtype under numpy's casting rules (statcounter.py:51-59), partitions are
+combined left to right with the Chan formula and its 10x size heuristic
+(statcounter.py:67-99), sum is elementwise `+` in the input dtype
+(array.py:269).
+"""
+import copy
+from functools import reduce as _reduce
+from itertools import product
+
+import numpy as np
+
+
+# ---------------------------------------------------------------- records
+class RecSet(object):
+    """Partitioned (key, value) records with bolt metadata (array.py:13-28)."""
+
+    def __init__(self, parts, shape, split, dtype):
+        self.parts = parts
+        self.shape = tuple(int(s) for s in shape)
+        self.split = int(split)
+        self.dtype = np.dtype(dtype)
+
+    def records(self):
+        return [kv for p in self.parts for kv in p]
+
+
+def _contiguous_parts(records, n):
+    L = len(records)
+    return [records[i * L // n:(i + 1) * L // n] for i in range(n)]
+
+
+def parallelize(x, axis=(0,), npartitions=2, dtype=None):
+    """ConstructSpark.array (spark/construct.py:43-70), quirk included:
+    records are taken from x.transpose(keys+values) but the shape stays x.shape."""
+    x = np.asarray(x) if dtype is None else np.asarray(x, dtype)
+    shape = x.shape
+    axes = (axis,) if isinstance(axis, int) else tuple(axis)
+    if min(axes) < 0 or max(axes) > len(shape) - 1:
+        raise ValueError("invalid key axes")
+    perm = list(axes) + [i for i in range(len(shape)) if i not in axes]
+    split = len(axes)
+    xt = x.transpose(perm)
+    kshape, vshape = shape[:split], shape[split:]
+    vals = xt.reshape((int(np.prod(kshape)),) + vshape)
+    keys = list(np.ndindex(*kshape))
+    recs = [(tuple(int(k) for k in key), vals[i]) for i, key in enumerate(keys)]
+    return RecSet(_contiguous_parts(recs, npartitions), shape, split, x.dtype)
+
+
+def toarray(rs):
+    """sortByKey + collect + reshape (array.py:1006-1014)."""
+    recs = sorted(rs.records(), key=lambda kv: kv[0])
+    return np.asarray([v for _, v in recs]).reshape(rs.shape)
+
+
+# ---------------------------------------------------------------- chunk plan
+def getplan(vshape, dtype, size="150", axes=None, padding=None):
+    """ChunkedArray.getplan (chunk.py:434-512)."""
+    vshape = np.asarray(vshape)
+    plan = vshape.copy()
+    if axes is None:
+        axes = np.arange(len(vshape)) if isinstance(size, str) else np.arange(len(size))
+    else:
+        axes = np.asarray(axes, 'int')
+    pad = np.zeros(len(vshape), dtype=int)
+    if padding is not None:
+        pad[axes] = padding
+    if isinstance(size, tuple):
+        plan[axes] = size
+    elif isinstance(size, str):
+        nbytes = 1000.0 * float(size)
+        item = np.dtype(dtype).itemsize
+        mask = np.zeros(len(vshape), dtype=bool)
+        mask[axes] = True
+        dims = vshape[mask]
+        if nbytes <= item:
+            s = np.ones(len(axes))
+        else:
+            rem = 1.0 * np.prod(vshape) * item
+            s = []
+            for i, d in enumerate(dims):
+                per = rem / d
+                if per >= nbytes:
+                    s.append(1)
+                    rem = per
+                    continue
+                s.append(min(d, np.floor(nbytes / per)))
+                s[i + 1:] = plan[i + 1:]
+                break
+        plan[axes] = s
+    else:
+        raise ValueError("Chunk size not understood")
+    return plan, pad
+
+
+def chunk_slices(plan, padding, vshape):
+    """getslices (chunk.py:574-618): full chunks get the right pad (clipped by
+    slicing), a remainder chunk is [floor(d/s)*s - p, d)."""
+    out = []
+    for s, p, d in zip(plan, padding, vshape):
+        s, p, d = int(s), int(p), int(d)
+        n, rem = d // s, d % s
+        sl = [slice(0 if j == 0 else j * s - p, j * s + s + p) for j in range(n)]
+        if rem:
+            sl.append(slice(n * s - p, d))
+        out.append(sl)
+    return out
+
+
+class ChunkSet(object):
+    """Chunk records ((key..., chunk id...), chunk) with plan/padding (chunk.py:11-33)."""
+
+    def __init__(self, parts, shape, split, dtype, plan, padding):
+        self.parts = parts
+        self.shape = tuple(int(s) for s in shape)
+        self.split = int(split)
+        self.dtype = np.dtype(dtype)
+        self.plan = np.asarray(plan, dtype=int)
+        self.padding = np.asarray(padding, dtype=int)
+
+    @property
+    def kshape(self):
+        return np.asarray(self.shape[:self.split])
+
+    @property
+    def vshape(self):
+        return np.asarray(self.shape[self.split:])
+
+    def records(self):
+        return [kv for p in self.parts for kv in p]
+
+
+def chunk(rs, size="150", axis=None, padding=None):
+    """BoltArraySpark.chunk -> ChunkedArray._chunk (array.py:678-714, chunk.py:87-144)."""
+    if not isinstance(size, str):
+        size = tuple(size) if isinstance(size, (tuple, list)) else (size,)
+    if axis is not None and not isinstance(axis, tuple):
+        axis = tuple(axis) if isinstance(axis, list) else (axis,)
+    if padding is not None and not isinstance(padding, tuple):
+        padding = tuple(padding) if isinstance(padding, list) else (padding,)
+    if rs.split == len(rs.shape) and padding is None:
+        parts = [[(k + (0,), np.array(v, ndmin=1)) for k, v in p] for p in rs.parts]
+        return ChunkSet(parts, rs.shape + (1,), rs.split, rs.dtype, (1,), [0])
+    vshape = rs.shape[rs.split:]
+    plan, pad = getplan(vshape, rs.dtype, size, axis, padding)
+    if any(x + y > z for x, y, z in zip(plan, pad, vshape)):
+        raise ValueError("Chunk sizes plus padding sizes cannot exceed value dimensions")
+    if any(x > y for x, y in zip(pad, plan)):
+        raise ValueError("Padding sizes cannot exceed chunk sizes")
+    sl = chunk_slices(plan, pad, vshape)
+    scheme = list(product(*[list(enumerate(s)) for s in sl]))
+    parts = []
+    for p in rs.parts:
+        q = []
+        for k, v in p:
+            for combo in scheme:
+                chk = tuple(c[0] for c in combo)
+                q.append((k + chk, v[tuple(c[1] for c in combo)]))
+        parts.append(q)
+    return ChunkSet(parts, rs.shape, rs.split, rs.dtype, plan, pad)
+
+
+def _nchunks(plan, vshape):
+    return [int(np.ceil(1.0 * d / s)) for s, d in zip(plan, vshape)]
+
+
+def _strip(idx, value, number, padding, axes):
+    """removepad (chunk.py:514-550), indexing with a tuple."""
+    sl = []
+    for a, (i, p, n) in enumerate(zip(idx, padding, number)):
+        m = (a in axes) and p != 0
+        lo = 0 if (i == 0 or not m) else p
+        hi = None if (i == n - 1 or not m) else -p
+        sl.append(slice(lo, hi))
+    return value[tuple(sl)]
+
+
+def _stack(nested):
+    """allstack (bolt/utils.py:193-208)."""
+    def go(v, depth):
+        if isinstance(v[0], np.ndarray):
+            return np.concatenate(v, axis=depth)
+        return np.concatenate([go(x, depth + 1) for x in v], axis=depth)
+    return go(nested, 0)
+
+
+def unchunk(cs):
+    """ChunkedArray.unchunk (chunk.py:146-200): strip padding, reassemble per key."""
+    split, vshape = cs.split, cs.vshape
+    number = _nchunks(cs.plan, vshape)
+    n = len(vshape)
+    recs = cs.records()
+    if np.any(cs.padding != 0):
+        recs = [(k, _strip(k[split:], v, number, cs.padding, range(n))) for k, v in recs]
+    if np.array_equal(cs.plan, vshape):
+        out = [(k[:split], v) for k, v in recs]
+    else:
+        groups = {}
+        for k, v in recs:
+            groups.setdefault(k[:split], []).append((k[split:], v))
+        out = []
+        for key in sorted(groups):
+            arr = np.empty(number, dtype=object)
+            for chk, v in groups[key]:
+                arr[chk] = v
+            out.append((key, _stack(arr.tolist())))
+    shape = cs.shape
+    if np.array_equal(vshape, [1]):
+        out = [(k, np.squeeze(v)) for k, v in out]
+        shape = shape[:-1]
+    return RecSet([out], shape, split, cs.dtype)
+
+
+def keys_to_values(cs, axes, size=None):
+    """ChunkedArray.keys_to_values (chunk.py:202-289): relabel, group by
+    (stationary keys, new chunk ids, old chunk ids), stack each group."""
+    if len(axes) == 0:
+        return cs
+    split = cs.split
+    kmask = np.zeros(split, dtype=bool)
+    kmask[list(axes)] = True
+    if size is None:
+        size = cs.kshape[kmask]
+    size = np.asarray(size, dtype=int)
+    newplan = np.r_[size, cs.plan]
+    newshape = tuple(np.r_[cs.kshape[~kmask], cs.kshape[kmask], cs.vshape].astype(int).tolist())
+    newpad = np.r_[np.zeros(len(axes), dtype=int), cs.padding]
+    groups = {}
+    for k, v in cs.records():
+        keys, chks = np.asarray(k[:split]), tuple(k[split:])
+        mov, sta = keys[kmask], keys[~kmask]
+        newchk = tuple(int(m) for m in mov // size)
+        label = tuple(int(m) for m in mov % size)
+        gk = tuple(int(s) for s in sta) + newchk + chks
+        groups.setdefault(gk, []).append((label, v))
+    out = []
+    for gk in sorted(groups):
+        items = sorted(groups[gk], key=lambda t: t[0])
+        labels = np.asarray([t[0] for t in items])
+        lshape = tuple(labels.max(axis=0) - labels.min(axis=0) + 1)
+        out.append((gk, np.asarray([t[1] for t in items]).reshape(lshape + items[0][1].shape)))
+    res = ChunkSet([out], newshape, split - len(axes), cs.dtype, newplan, newpad)
+    if np.array_equal(cs.vshape, [1]):
+        # squeeze the all-keys singleton (chunk.py:284-287, numpy<1.13 semantics)
+        res.parts = [[(k[:-1], np.squeeze(v)) for k, v in out]]
+        res.shape = res.shape[:-1]
+        res.plan = res.plan[:-1]
+        res.padding = res.padding[:len(res.plan)]
+    return res
+
+
+def values_to_keys(cs, axes):
+    """ChunkedArray.values_to_keys (chunk.py:291-347): strip padding on the
+    moved axes, emit one record per index of the moved dims."""
+    split = cs.split
+    nv = len(cs.vshape)
+    vmask = np.zeros(nv, dtype=bool)
+    vmask[list(axes)] = True
+    newplan = cs.plan[~vmask]
+    newshape = tuple(np.r_[cs.kshape, cs.vshape[vmask], cs.vshape[~vmask]].astype(int).tolist())
+    newpad = cs.padding[~vmask]
+    number = _nchunks(cs.plan, cs.vshape)
+    moving = cs.plan[vmask]
+    out = []
+    for k, v in cs.records():
+        key, chk = k[:split], np.asarray(k[split:])
+        if np.any(cs.padding != 0):
+            v = _strip(tuple(chk), v, number, cs.padding, list(axes))
+        offs = chk[vmask] * moving
+        for b in np.ndindex(*np.asarray(v.shape)[vmask]):
+            sl = [slice(None)] * nv
+            for a, bi in zip(np.flatnonzero(vmask), b):
+                sl[a] = bi
+            nk = tuple(int(x) for x in key) + tuple(int(o + bi) for o, bi in zip(offs, b))
+            out.append((nk + tuple(int(c) for c in chk[~vmask]), v[tuple(sl)]))
+    res = ChunkSet([out], newshape, split + len(axes), cs.dtype, newplan, newpad)
+    if len(newshape) == split + len(axes):
+        res.parts = [[(k, np.array(v, ndmin=1)) for k, v in out]]
+        res.shape = res.shape + (1,)
+        res.plan = np.array([1])
+        res.padding = np.array([0])
+    return res
+
+
+# ---------------------------------------------------------------- swap etc.
+def swap(rs, kaxes, vaxes, size="150"):
+    """BoltArraySpark.swap (array.py:716-763) through the chunk machinery."""
+    kaxes = [int(k) for k in np.atleast_1d(np.asarray(kaxes, dtype=int))]
+    vaxes = [int(v) for v in np.atleast_1d(np.asarray(vaxes, dtype=int))]
+    if len(kaxes) == rs.split and len(vaxes) == 0:
+        raise ValueError('Cannot perform a swap that would end up with all data on a single key')
+    if len(kaxes) == 0 and len(vaxes) == 0:
+        return rs
+    c = chunk(rs, size)
+    c = keys_to_values(c, kaxes)
+    c = values_to_keys(c, [v + len(kaxes) for v in vaxes])
+    return unchunk(c)
+
+
+def _keys_permute(rs, p):
+    recs = [(tuple(k[i] for i in p), v) for k, v in rs.records()]
+    shape = tuple(rs.shape[i] for i in p) + rs.shape[rs.split:]
+    return RecSet([sorted(recs, key=lambda kv: kv[0])], shape, rs.split, rs.dtype)
+
+
+def _values_permute(rs, p):
+    recs = [(k, v.transpose(p)) for k, v in rs.records()]
+    shape = rs.shape[:rs.split] + tuple(rs.shape[rs.split + i] for i in p)
+    return RecSet([recs], shape, rs.split, rs.dtype)
+
+
+def transpose(rs, p):
+    """BoltArraySpark.transpose (array.py:765-808): swap the crossing axes,
+    then permute keys (shapes.py:66-89) and values (shapes.py:136-159)."""
+    p = np.asarray(p)
+    split = rs.split
+    nk, nv = p[:split], p[split:]
+    sk = np.sort(nv[nv < split])
+    sv = np.sort(nk[nk >= split])
+    stk = np.sort(nk[nk < split])
+    stv = np.sort(nv[nv >= split])
+    pswap = np.r_[stk, sv, sk, stv]
+    px = np.argsort(pswap)[p]
+    out = swap(rs, sk, sv - split) if (len(sk) or len(sv)) else rs
+    out = _keys_permute(out, [int(i) for i in px[:split]])
+    return _values_permute(out, [int(i) - split for i in px[split:]])
+
+
+# ---------------------------------------------------------------- statistics
+class StatCounter(object):
+    """statcounter.py:28-130 (Welford merge, Chan combine), in the record dtype."""
+
+    def __init__(self, values=(), need_m2=True):
+        self.n = 0
+        self.mu = 0.0
+        self.m2 = 0.0
+        self.need_m2 = need_m2
+        for v in values:
+            self.merge(v)
+
+    def merge(self, value):
+        self.n += 1
+        delta = value - self.mu
+        self.mu += delta / self.n
+        if self.need_m2:
+            self.m2 += delta * (value - self.mu)
+        return self
+
+    def combine(self, other):
+        if other is self:
+            return self.merge(copy.deepcopy(other))
+        if self.n == 0:
+            self.n, self.mu, self.m2 = other.n, other.mu, other.m2
+        elif other.n != 0:
+            delta = other.mu - self.mu
+            if other.n * 10 < self.n:
+                self.mu = self.mu + (delta * other.n) / (self.n + other.n)
+            elif self.n * 10 < other.n:
+                self.mu = other.mu - (delta * self.n) / (self.n + other.n)
+            else:
+                self.mu = (self.mu * self.n + other.mu * other.n) / (self.n + other.n)
+            if self.need_m2:
+                self.m2 += other.m2 + (delta * delta * self.n * other.n) / (self.n + other.n)
+            self.n += other.n
+        return self
+
+    def stat(self, name):
+        if name == 'mean':
+            return self.mu
+        var = float('nan') if self.n == 0 else self.m2 / self.n
+        return var if name == 'variance' else np.sqrt(var)
+
+
+def align(rs, axis):
+    """BoltArraySpark._align (array.py:85-115): reduced axes become the keys."""
+    if not all(0 <= a < len(rs.shape) for a in axis):
+        raise ValueError("axes not valid for an ndarray of shape: %s" % str(rs.shape))
+    tokeys = [a - rs.split for a in axis if a >= rs.split]
+    tovalues = [a for a in range(rs.split) if a not in axis]
+    if tokeys or tovalues:
+        return swap(rs, tovalues, tokeys)
+    return rs
+
+
+def _normalise_axis(rs, axis):
+    if axis is None:
+        axis = list(range(len(rs.shape)))
+    return tuple(axis) if isinstance(axis, (tuple, list)) else (axis,)
+
+
+def stat(rs, name, axis=None, keepdims=False):
+    """BoltArraySpark._stat with a name (array.py:284-334): one StatCounter per
+    partition, combined in partition order; a 0-d result becomes a scalar."""
+    axis = _normalise_axis(rs, axis)
+    sw = align(rs, axis)
+    counters = [StatCounter((v for _, v in p), need_m2=(name != 'mean')) for p in sw.parts]
+    arr = _reduce(lambda a, b: a.combine(b), counters).stat(name)
+    if keepdims:
+        for i in axis:
+            arr = np.expand_dims(arr, axis=i)
+    arr = np.asarray(arr) if not np.isscalar(arr) else arr
+    if isinstance(arr, np.ndarray) and arr.shape == ():
+        return arr.reshape(1)[0]
+    return arr
+
+
+def sum_(rs, axis=None, keepdims=False):
+    """BoltArraySpark.reduce(add) (array.py:243-282): treeReduce of `+` in the input dtype."""
+    axis = _normalise_axis(rs, axis)
+    sw = align(rs, axis)
+    partials = [_reduce(lambda a, b: a + b, [v for _, v in p]) for p in sw.parts if p]
+    arr = _reduce(lambda a, b: a + b, partials)
+    if keepdims:
+        for i in axis:
+            arr = np.expand_dims(arr, axis=i)
+    if not isinstance(arr, np.ndarray):
+        return arr
+    if arr.shape == (1,):
+        return arr[0]
+    return arr
+
+
+def repartition(rs, n):
+    """Records in key order split into n contiguous partitions (parallelize's cut)."""
+    recs = sorted(rs.records(), key=lambda kv: kv[0])
+    return RecSet(_contiguous_parts(recs, n), rs.shape, rs.split, rs.dtype)

@@ -1,0 +1,360 @@
+"""Generate the golden fixtures from the REFERENCE bolt (Spark mode).
+
+Run in the build container only (it imports /root/reference, which is not on
+the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference's Spark path runs over fakespark/ (an in-process RDD, see
+fakerdd.py) with two shims for behaviour the reference relied on from old
+numpy:
+  * ChunkedArray.removepad indexes with tuple(slices) (chunk.py:550 passes a
+    list, which numpy >= 1.23 rejects);
+  * after keys_to_values squeezes the all-keys singleton value axis
+    (chunk.py:284-287) the padding and the stale trailing chunk id are
+    trimmed, as numpy < 1.13's short boolean masks did.
+Writes tests/golden/golden.json (case specs + scalar results) and
+tests/golden/golden.npz (output arrays).  Inputs are regenerated from specs
+(tests/golden/inputs.py).
+"""
+import collections
+import collections.abc
+import json
+import os
+import sys
+import traceback
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("BOLT_REFERENCE", "/root/reference")
+sys.path[:0] = [REF, os.path.join(HERE, "fakespark"), HERE]
+collections.Iterable = collections.abc.Iterable  # bolt/utils.py:3 on Python >= 3.10
+
+import numpy as np  # noqa: E402
+
+import bolt  # noqa: E402
+from bolt.spark.chunk import ChunkedArray  # noqa: E402
+from fakerdd import FakeContext  # noqa: E402
+from inputs import make_input  # noqa: E402
+
+
+# ---------------------------------------------------------------- shims
+def _removepad(idx, value, number, padding, axes=None):
+    if axes is None:
+        axes = range(len(number))
+    mask = len(number) * [False, ]
+    for i in range(len(mask)):
+        if i in axes and padding[i] != 0:
+            mask[i] = True
+    starts = [0 if (i == 0 or not m) else p for (i, m, p) in zip(idx, mask, padding)]
+    stops = [None if (i == n - 1 or not m) else -p for (i, m, p, n) in zip(idx, mask, padding, number)]
+    slices = [slice(i1, i2) for (i1, i2) in zip(starts, stops)]
+    return value[tuple(slices)]
+
+
+ChunkedArray.removepad = staticmethod(_removepad)
+_k2v = ChunkedArray.keys_to_values
+
+
+def _keys_to_values(self, axes, size=None):
+    res = _k2v(self, axes, size)
+    if res is not self and len(res._padding) > len(res._plan):
+        res._padding = res._padding[:len(res._plan)]
+        res._rdd = res._rdd.map(lambda kv: (kv[0][:-1], kv[1]))
+    return res
+
+
+ChunkedArray.keys_to_values = _keys_to_values
+
+
+# ---------------------------------------------------------------- cases
+CASES = []
+ARRAYS = {}
+
+
+def add(case, **arrays):
+    i = len(CASES)
+    case["id"] = i
+    for k, v in arrays.items():
+        ARRAYS["c%d_%s" % (i, k)] = np.asarray(v)
+    case["arrays"] = sorted(arrays)
+    CASES.append(case)
+
+
+def spec(shape, dtype="int64", kind="arange", seed=0, **kw):
+    d = {"shape": list(shape), "dtype": str(np.dtype(dtype)), "kind": kind, "seed": seed}
+    d.update(kw)
+    return d
+
+
+def run(fn, case):
+    try:
+        return fn()
+    except Exception as e:  # record the exception type as the golden result
+        case["raises"] = type(e).__name__
+        return None
+
+
+def gen_construct():
+    for sh, axis, npart in [((2, 3, 4), (0,), None), ((2, 3, 4), (0, 1), 5), ((2, 3, 4), (0, 1, 2), None),
+                            ((2, 3, 4), (1,), None), ((2, 3, 4), (2, 0), None), ((4, 5, 6), (1, 2), 3),
+                            ((2, 3, 4), (-1,), None), ((2, 3, 4), (0, 1, 2, 3), None)]:
+        s = spec(sh)
+        x = make_input(s)
+        case = {"op": "construct", "input": s, "axis": list(axis), "npartitions": npart}
+        b = run(lambda: bolt.array(x, sc, axis=axis, npartitions=npart), case)
+        if b is None:
+            add(case)
+            continue
+        case.update(shape=list(b.shape), split=b.split)
+        add(case, out=b.toarray())
+
+
+def gen_swap():
+    items = [
+        (spec([2] * 8), (0, 1, 2, 3), (1, 2), (0, 3), (2, 2)),
+        (spec([2] * 8), (0, 1, 2, 3), (1, 2), (0, 3), "50"),
+        (spec([2] * 8), (0, 1, 2, 3), (1, 2), (0, 3), "150"),
+        (spec([2] * 8), (0, 1, 2, 3), (), (0, 1, 2, 3), "150"),
+        (spec([2] * 8), (0, 1, 2, 3), (0,), (0,), "150"),
+        (spec([2] * 8), (0, 1, 2, 3), (), (0,), "150"),
+        (spec([2] * 8), (0, 1, 2, 3), (0,), (), "150"),
+        (spec([2] * 8), tuple(range(8)), (0, 1), (), "150"),
+        (spec((2, 3, 4)), (0,), (0,), (0, 1), "150"),
+        (spec((2, 3, 4)), (0,), (0,), (), "150"),
+        (spec((2, 3, 4)), (0,), (), (), "150"),
+        (spec((50, 32, 32), "float64", "normal", 0), (0,), (0,), (0,), "150"),         # C1 scaled
+        (spec((20, 16, 16), "float32", "imaging", 1), (0,), (0,), (0, 1), "150"),     # C2 scaled
+        (spec((16, 8, 8, 4), "float32", "bits", 2), (0, 1), (0,), (0,), "150"),       # C3 scaled
+        (spec((16, 8, 8, 4), "float32", "bits", 2), (0, 1), (0,), (0,), "150000"),
+        (spec((16, 8, 8, 4), "float32", "bits", 2), (0, 1), (1,), (0,), "150"),
+        (spec((30, 40, 24), "uint16", "ints", 3), (0,), (0,), (0,), "0.5"),           # C4 scaled
+        (spec((4, 4, 4, 6, 6), "float64", "normal", 4), (0, 1, 2), (0, 2), (1,), "0.1"),  # C5 scaled
+        (spec((4, 4, 4, 6, 6), "float64", "normal", 4), (0, 1, 2), (1,), (0, 1), (2, 3)),
+        (spec((3, 5, 7), "bool", "bool", 5), (0,), (0,), (1,), "150"),
+        (spec((6, 10), "int8", "ints", 6), (0,), (0,), (0,), (4,)),
+        (spec((2, 3, 4)), (0, 1), (0, 1), (), "150"),    # all keys, no values: error
+        (spec((2, 3, 4)), (0,), (0,), (0,), (5, 5)),     # plan > vshape: error
+    ]
+    for s, axis, kax, vax, size in items:
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=axis)
+        case = {"op": "swap", "input": s, "axis": list(axis), "kaxes": list(kax), "vaxes": list(vax),
+                "size": size if isinstance(size, str) else list(size)}
+        r = run(lambda: b.swap(kax, vax, size=size), case)
+        if r is None:
+            add(case)
+            continue
+        case.update(shape=list(r.shape), split=r.split)
+        add(case, out=r.toarray())
+
+
+def gen_transpose():
+    from itertools import permutations
+    s = spec((2, 3, 4, 5))
+    x = make_input(s)
+    for axis in [(0, 1), (0,), (0, 1, 2)]:
+        b = bolt.array(x, sc, axis=axis)
+        for p in permutations(range(4)):
+            case = {"op": "transpose", "input": s, "axis": list(axis), "perm": list(p)}
+            r = b.transpose(p)
+            case.update(shape=list(r.shape), split=r.split)
+            add(case, out=r.toarray())
+    for s2, axis in [(spec((4, 4, 4, 6, 6), "float64", "normal", 4), (0, 1, 2)),
+                     (spec((16, 8, 8, 4), "float32", "bits", 2), (0, 1))]:
+        x2 = make_input(s2)
+        b = bolt.array(x2, sc, axis=axis)
+        for name, f in [("T", lambda b: b.T), ("perm20413", lambda b: b.transpose(2, 0, 4, 1, 3) if b.ndim == 5 else b.transpose(3, 1, 0, 2)),
+                        ("swapaxes", lambda b: b.swapaxes(0, b.ndim - 1))]:
+            case = {"op": "transpose_named", "input": s2, "axis": list(axis), "name": name}
+            r = f(b)
+            case.update(shape=list(r.shape), split=r.split)
+            add(case, out=r.toarray())
+    b = bolt.array(x, sc, axis=(0, 1))
+    for bad in [(0, 1, 1, 2), (0, 1, 2), (0, 1, 2, 4)]:
+        case = {"op": "transpose", "input": s, "axis": [0, 1], "perm": list(bad)}
+        run(lambda: b.transpose(bad), case)
+        add(case)
+
+
+def _records(chunked):
+    recs = chunked.tordd().sortByKey().collect()
+    keys = [[int(k) for k in kk] for kk, _ in recs]
+    shapes = [list(v.shape) for _, v in recs]
+    flat = np.concatenate([np.asarray(v).reshape(-1) for _, v in recs]) if recs else np.zeros(0)
+    return keys, shapes, flat
+
+
+def gen_chunk():
+    items = [
+        (spec((1, 4, 6)), (0,), (2, 3), None, None),
+        (spec((1, 4, 6)), (0,), (3, 4), None, None),
+        (spec((1, 4, 6)), (0,), (4, 6), None, None),
+        (spec((1, 4, 6)), (0,), "0.1", None, None),
+        (spec((1, 4, 6)), (0,), "150", None, None),
+        (spec((1, 4, 5, 10)), (0,), (3, 3, 3), None, None),
+        (spec((1, 4, 5, 10)), (0,), (1, 1, 1), None, None),
+        (spec((4, 6)), (0, 1), (), None, None),
+        (spec((4, 6)), (0,), 2, None, None),
+        (spec((2, 2, 5, 6)), (0, 1), (2, 2), None, 1),
+        (spec((2, 2, 5, 6)), (0, 1), (3, 3), None, (1, 2)),
+        (spec((2, 2, 5, 6)), (0, 1), (2, 2), None, (3, 1)),   # error
+        (spec((2, 2, 5, 6)), (0, 1), (4, 4), None, (2, 2)),   # error
+        (spec((1, 4, 6)), (0,), (5, 6), None, None),          # error
+        (spec((3, 12, 12), "float64", "normal", 7), (0,), (4, 4), None, 2),    # C5-like padded
+        (spec((3, 10, 9), "float64", "normal", 7), (0,), (4, 4), None, (1, 2)),
+        (spec((3, 10, 9), "uint16", "ints", 8), (0,), (3,), (1,), None),       # axis subset (tuple size)
+        (spec((5, 20, 30), "uint16", "ints", 9), (0,), "0.5", None, None),     # C4-like ragged plan
+        (spec((2, 3, 64, 64), "float64", "normal", 10), (0, 1), (16, 16), None, 2),
+    ]
+    for s, axis, size, caxis, pad in items:
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=axis)
+        case = {"op": "chunk", "input": s, "axis": list(axis),
+                "size": size if isinstance(size, str) else (list(size) if isinstance(size, tuple) else size),
+                "chunk_axis": caxis if caxis is None else list(caxis),
+                "padding": pad if not isinstance(pad, tuple) else list(pad)}
+        c = run(lambda: b.chunk(size, axis=caxis, padding=pad), case)
+        if c is None:
+            add(case)
+            continue
+        keys, shapes, flat = _records(c)
+        case.update(keys=keys, shapes=shapes, plan=[int(p) for p in c.plan],
+                    padding_out=[int(p) for p in c.padding], uniform=bool(c.uniform),
+                    chunk_shape=list(c.shape), split=c.split)
+        u = c.unchunk()
+        case.update(unchunk_shape=list(u.shape), unchunk_split=u.split)
+        sub = {}
+        arr = run(lambda: u.toarray(), sub)
+        if arr is None:
+            # the reference's removepad trims a full p from a clipped chunk
+            # when 0 < d % s < p (chunk.py:546-547 vs getslices' clipping)
+            case["unchunk_raises"] = sub["raises"]
+            add(case, flat=flat)
+            continue
+        add(case, flat=flat, unchunk=arr)
+
+
+def gen_moves():
+    """keys_to_values / values_to_keys chains (test_spark_chunking.py:51-112 and more)."""
+    items = [
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("k2v", (0,), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("k2v", (1,), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("k2v", (1,), (3,))]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("k2v", (0, 1), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("k2v", (0, 1), (2, 3))]),
+        (spec((4, 7, 9, 6)), (0, 1, 2, 3), (), None, [("k2v", (3,), None)]),
+        (spec((4, 7, 9, 6)), (0, 1, 2, 3), (), None, [("k2v", (0, 1), None)]),
+        (spec((4, 7, 9, 6)), (0,), (2, 3, 4), None, [("k2v", (0,), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("v2k", (0,), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("v2k", (1,), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("v2k", (0, 1), None)]),
+        (spec((4, 7, 9, 6)), (0, 1), (4, 2), None, [("v2k", (), None)]),
+        (spec((4, 7, 9, 6)), (0,), (2, 3, 4), None, [("v2k", (0,), None)]),
+        (spec((4, 7, 9, 6)), (0,), (2, 3, 4), None, [("v2k", (0, 1), None)]),
+        (spec((2, 2, 5, 6)), (0, 1), (2, 2), 1, [("k2v", (1,), None)]),
+        (spec((2, 2, 5, 6)), (0, 1), (2, 2), 1, [("v2k", (0,), None)]),
+        (spec((3, 4, 9, 10), "float64", "normal", 11), (0, 1), (4, 4), (1, 2), [("k2v", (0,), None), ("v2k", (1,), None)]),
+        (spec((3, 4, 9, 10), "float64", "normal", 11), (0, 1), (4, 4), 2, [("v2k", (0, 1), None), ("k2v", (1, 2), (2, 3))]),
+    ]
+    for s, axis, size, pad, steps in items:
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=axis)
+        c = b.chunk(size, padding=pad)
+        case = {"op": "moves", "input": s, "axis": list(axis),
+                "size": list(size) if isinstance(size, tuple) else size,
+                "padding": list(pad) if isinstance(pad, tuple) else pad,
+                "steps": [[n, list(a), (list(z) if z is not None else None)] for n, a, z in steps]}
+        def apply(c):
+            for n, a, z in steps:
+                c = c.keys_to_values(a, size=z) if n == "k2v" else c.values_to_keys(a)
+            return c, _records(c)
+        res = run(lambda: apply(c), case)
+        if res is None:
+            add(case)
+            continue
+        c, (keys, shapes, flat) = res
+        case.update(keys=keys, shapes=shapes, plan=[int(p) for p in c.plan],
+                    padding_out=[int(p) for p in c.padding], chunk_shape=[int(q) for q in c.shape],
+                    split=c.split)
+        u = c.unchunk()
+        case.update(unchunk_shape=list(u.shape), unchunk_split=u.split)
+        add(case, flat=flat, unchunk=u.toarray())
+
+
+def gen_getplan():
+    cfg = [((512, 512), "float32", "150"), ((256, 256, 32), "float32", "150"), ((256, 32), "float32", "150"),
+           ((256, 32), "float32", "150000"), ((1024, 1024), "uint16", "150"), ((64, 64), "float64", "150"),
+           ((64, 64), "float64", "150000"), ((5, 6), "int64", "0.1"), ((5, 6), "int64", "0.001"),
+           ((7, 9, 11), "float64", "1"), ((3, 4, 5), "uint8", "0.02")]
+    for vs, dt, size in cfg:
+        x = np.zeros((1,) + vs, dtype=dt)
+        b = bolt.array(x, sc)
+        c = b.chunk(size)
+        add({"op": "getplan", "vshape": list(vs), "dtype": dt, "size": size,
+             "plan": [int(p) for p in c.plan], "padding_out": [int(p) for p in c.padding]})
+
+
+def gen_stats():
+    inputs = [
+        (spec((2, 3, 4)), (0,)),
+        (spec((2, 3, 4), "float64", "normal", 12), (0,)),
+        (spec((2, 3, 4), "float64", "normal", 12), (0, 1)),
+        (spec((6, 5, 7), "float32", "imaging", 13), (0,)),
+        (spec((6, 5, 7), "float32", "normal", 13), (0, 1)),
+        (spec((9, 4, 3), "uint16", "ints", 14), (0,)),
+        (spec((9, 4, 3), "int32", "ints", 15, small=1), (0,)),
+        (spec((5, 4), "bool", "bool", 16), (0,)),
+        (spec((100, 64, 64), "float64", "normal", 0), (0,)),   # C1
+    ]
+    axes_list = [None, 0, 1, 2, (0, 1), (0, 2), (1, 2), (0, 1, 2)]
+    for s, kaxis in inputs:
+        x = make_input(s)
+        for npart in ((8,) if s["shape"] == [100, 64, 64] else (1, 2, 8)):
+            b = bolt.array(x, sc, axis=kaxis, npartitions=npart)
+            for name in ("mean", "var", "std", "sum"):
+                for ax in axes_list:
+                    if ax is not None and max(np.atleast_1d(ax)) >= x.ndim:
+                        continue
+                    for keep in (False, True):
+                        if keep and ax not in (None, 1, (0, 2)):
+                            continue
+                        if npart != 2 and s["shape"] != [100, 64, 64] and (ax not in (None, 0, (0, 1))):
+                            continue
+                        case = {"op": "stat", "input": s, "axis": list(kaxis), "npartitions": npart,
+                                "name": name, "reduce_axis": ax if not isinstance(ax, tuple) else list(ax),
+                                "keepdims": keep}
+                        r = run(lambda: getattr(b, name)(axis=ax, keepdims=keep), case)
+                        if r is None and "raises" in case:
+                            add(case)
+                            continue
+                        case["result_type"] = type(r).__name__
+                        case["result_dtype"] = str(np.asarray(r).dtype)
+                        add(case, out=np.asarray(r))
+
+
+def gen_stat_errors():
+    s = spec((2, 3, 4))
+    x = make_input(s)
+    b = bolt.array(x, sc, axis=(0,))
+    for ax in [3, (0, 3), -1]:
+        case = {"op": "stat", "input": s, "axis": [0], "npartitions": None, "name": "mean",
+                "reduce_axis": ax if not isinstance(ax, tuple) else list(ax), "keepdims": False}
+        run(lambda: b.mean(axis=ax), case)
+        add(case)
+
+
+if __name__ == "__main__":
+    sc = FakeContext(2)
+    for g in (gen_construct, gen_swap, gen_transpose, gen_chunk, gen_moves, gen_getplan, gen_stats,
+              gen_stat_errors):
+        try:
+            g()
+        except Exception:
+            traceback.print_exc()
+            raise
+    meta = {"generator": "tests/golden/make_golden.py", "reference": "beautifulNow1992/bolt v%s" % bolt.__version__,
+            "numpy": np.__version__, "python": sys.version.split()[0], "cases": CASES}
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, indent=0, sort_keys=True)
+    np.savez_compressed(os.path.join(HERE, "golden.npz"), **ARRAYS)
+    print("wrote %d cases, %d arrays" % (len(CASES), len(ARRAYS)))
