@@ -1,0 +1,256 @@
+"""Benchmark of the mi355x mode's hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|target64]
+
+One "step" = one pass of the hot path over one batch of synthetic input,
+resident in HBM before timing starts.  Default workload (BASELINE.json
+configs[1], "C2"): float32 (2000, 512, 512) time series per GPU, key = time
+(split 1); swap((0,), (0,1)) to key = voxel, then mean and std over time
+(axis 2) -- the three calls a bolt user makes, each returning its result to
+the host as the reference does.
+
+`value` = algorithmic bytes of all ranks / wall time of K steps (max over
+ranks), GB/s:  swap 2*N*s, each stat N*s + outputs.  `roofline` is the
+dominant kernel (the swap's permute) measured with hipEvents on the stream it
+runs on; `cpu_baseline` times the oracle's record-level restatement of the
+reference Spark path (oracle/bolt_oracle.py) on a bounded sample on the host.
+
+For N > 1 (torch.distributed.run, one rank per GPU, RCCL): weak scaling, the
+time axis grows with N (2000*N), the swap becomes pack -> all-to-all ->
+unpack, the statistics reduce locally and all_gather their outputs.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBPS = 153.0      # per link, per direction
+
+CONFIGS = {
+    # name: (per-GPU shape, dtype, split, description)
+    "C2": ((2000, 512, 512), np.float32, 1,
+           "C2: float32 (2000,512,512) per GPU, key=time; swap((0,),(0,1)) + mean/std over time"),
+    "C3": ((4096, 256, 256, 32), np.float32, 2,
+           "C3: float32 (4096,256,256,32) per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
+    "C4": ((10000, 1024, 1024), np.uint16, 1,
+           "C4: uint16 (10000,1024,1024) per GPU, key 0; swap((0,),(0,)) + var over axis 0"),
+    "C5": ((64, 64, 64, 64, 64), np.float64, 3,
+           "C5: float64 64^5 per GPU, keys (0,1,2); .T + mean/std over axis 0"),
+    "target64": ((8192, 256, 256, 32), np.float32, 2,
+                 "64 GiB float32 4-D per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=None)
+    return ap.parse_args()
+
+
+def synth_shard(torch, shape, dtype, device, seed):
+    """Synthetic input generated in HBM (no host copy): imaging-like floats or random ints."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    if np.dtype(dtype) == np.float32:
+        t = torch.randn(shape, generator=g, device=device, dtype=torch.float32)
+        return t.mul_(50.0).add_(1000.0)
+    if np.dtype(dtype) == np.float64:
+        return torch.randn(shape, generator=g, device=device, dtype=torch.float64)
+    if np.dtype(dtype) == np.uint16:
+        t = torch.randint(0, 65536, shape, generator=g, device=device, dtype=torch.int32)
+        return t.to(torch.int16)  # same bits as uint16
+    raise ValueError(dtype)
+
+
+def workload(cfg, b):
+    """The step for a config: returns (swapped, [stat results])."""
+    if cfg == "C2":
+        s = b.swap((0,), (0, 1))
+        return s, [s.mean(axis=2), s.std(axis=2)]
+    if cfg in ("C3", "target64"):
+        s = b.swap((0,), (0,))
+        return s, [b.mean(axis=0), b.std(axis=0)]
+    if cfg == "C4":
+        s = b.swap((0,), (0,))
+        return s, [b.var(axis=0)]
+    if cfg == "C5":
+        s = b.T
+        return s, [b.mean(axis=0), b.std(axis=0)]
+    raise ValueError(cfg)
+
+
+def step_bytes(cfg, global_shape, dtype):
+    n = int(np.prod(global_shape))
+    s = np.dtype(dtype).itemsize
+    if cfg == "C2":
+        out = global_shape[1] * global_shape[2]
+        ob = np.dtype(np.float32).itemsize
+        return {"swap": 2 * n * s, "mean": n * s + out * ob, "std": n * s + out * ob}
+    if cfg in ("C3", "target64", "C5"):
+        out = n // global_shape[0]
+        ob = s
+        return {"swap": 2 * n * s, "mean": n * s + out * ob, "std": n * s + out * ob}
+    if cfg == "C4":
+        out = n // global_shape[0]
+        return {"swap": 2 * n * s, "var": n * s + out * 8}
+    raise ValueError(cfg)
+
+
+def cpu_baseline(cfg, shape, dtype, rows):
+    """Oracle (record-level restatement of the reference Spark path), 1 core, bounded sample."""
+    from oracle import bolt_oracle as O
+    if cfg != "C2":
+        return None
+    rng = np.random.default_rng(0)
+    sample_shape = (rows,) + tuple(shape[1:])
+    x = (1000 + 50 * rng.standard_normal(sample_shape)).astype(dtype)
+    rs = O.parallelize(x, axis=(0,), npartitions=8)
+    t0 = time.perf_counter()
+    s = O.swap(rs, (0,), (0, 1))
+    t1 = time.perf_counter()
+    O.stat(s, 'mean', axis=2)
+    t2 = time.perf_counter()
+    O.stat(s, 'stdev', axis=2)
+    t3 = time.perf_counter()
+    b = step_bytes(cfg, sample_shape, dtype)
+    total = sum(b.values())
+    return {"value": total / (t3 - t0) / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s: "
+                      "swap((0,),(0,1)) %.2fs + mean(axis=2) %.2fs + std(axis=2) %.2fs"
+                      % (str(sample_shape), t1 - t0, t2 - t1, t3 - t2),
+            "host_cpus": os.cpu_count()}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import bolt_amd as bolt
+    from bolt_amd import MI355XContext
+    ctx = MI355XContext(device=dev)
+    assert ctx.world_size == world
+
+    shape, dtype, split, desc = CONFIGS[args.config]
+    gshape = (shape[0] * world,) + tuple(shape[1:])
+    shard = synth_shard(torch, shape, dtype, dev, 1234 + rank)
+    b = bolt.ConstructMI355X.fromshards(shard, gshape, context=ctx, split=split, dtype=dtype)
+    del shard
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        s, stats = workload(args.config, b)
+        del s, stats
+    barrier()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        s = workload_swap = None
+        if args.config == "C2":
+            s = b.swap((0,), (0, 1))
+            ev[i][1].record(stream)
+            s.mean(axis=2)
+            s.std(axis=2)
+        elif args.config in ("C3", "target64"):
+            s = b.swap((0,), (0,))
+            ev[i][1].record(stream)
+            b.mean(axis=0)
+            b.std(axis=0)
+        elif args.config == "C4":
+            s = b.swap((0,), (0,))
+            ev[i][1].record(stream)
+            b.var(axis=0)
+        else:
+            s = b.T
+            ev[i][1].record(stream)
+            b.mean(axis=0)
+            b.std(axis=0)
+        del s, workload_swap
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    swap_ms = float(np.mean([a.elapsed_time(z) for a, z in ev]))
+    per = step_bytes(args.config, gshape, dtype)
+    total = sum(per.values()) * args.steps
+    value = total / elapsed / 1e9
+    swap_bytes_rank = per["swap"] / world
+    achieved = swap_bytes_rank / (swap_ms / 1e3) / 1e9
+
+    line = {
+        "metric": "swap/transpose GB/s + stat-reduce GB/s, % of HBM/xGMI roofline, 1-8 GPUs",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"float32": "f32", "float64": "f64", "uint16": "u16"}[np.dtype(dtype).name],
+        "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
+        "config": {"workload": desc, "global_shape": list(gshape), "split": split,
+                   "parallelism": "dp%d (records sharded on the leading key axis)" % world,
+                   "bytes_per_step": {k: int(v) for k, v in per.items()}},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_transpose (bm_permute) for the swap" if world == 1 else
+                      "swap = pack + RCCL all_to_all + unpack (per rank)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": None,
+            "avg_ms": round(swap_ms, 4),
+            "bytes_per_launch": int(swap_bytes_rank),
+        },
+    }
+    if world > 1:
+        G = world
+        payload = per["swap"] / 2 * (G - 1) / G / G  # bytes each rank sends to peers
+        line["roofline"]["xgmi"] = {"peak_GBps_per_rank": (G - 1) * XGMI_LINK_GBPS,
+                                    "payload_bytes_per_rank": int(payload)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rows = args.cpu_sample_rows or 128
+        line["cpu_baseline"] = cpu_baseline(args.config, shape, dtype, rows)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+"""A numpy executor of the libbolt_mi355x kernel contracts, for CPU tests only.
+
+The product has no CPU fallback (bolt_amd.mi355x._ops raises for a non-GPU
+device).  Tests register this executor for the 'cpu' device type to check the
+HOST logic -- chunk geometry and copy descriptors, swap/transpose planning,
+reduction layouts, result formatting and the multi-rank orchestration over
+gloo -- with world sizes > 1 on a machine without a GPU.  It implements each
+C-ABI entry point's documented semantics (include/bolt_mi355x.h) with numpy:
+strided copies through np.ndarray views, reductions in float64/longdouble
+with the same output-dtype and modular-integer rules as the kernels.
+"""
+import numpy as np
+
+STAT_MEAN, STAT_VAR, STAT_STD, STAT_SUM = range(4)
+_CODES = [np.bool_, np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64,
+          np.int64, np.float16, np.float32, np.float64]
+
+
+def _np(t):
+    return t.numpy()
+
+
+def _view(buf, off, shape, strides, es):
+    return np.ndarray(tuple(int(s) for s in shape), dtype=np.dtype((np.void, es)), buffer=buf,
+                      offset=int(off), strides=tuple(int(s) * es for s in strides))
+
+
+class CpuBackend(object):
+    name = "cpu-test"
+
+    def copy_strided(self, src, src_off, dst, dst_off, shape, sstrides, dstrides, es):
+        if len(shape) == 0:
+            shape, sstrides, dstrides = [1], [1], [1]
+        if any(int(s) == 0 for s in shape):
+            return
+        s = _view(_np(src), src_off, shape, sstrides, es)
+        d = _view(_np(dst), dst_off, shape, dstrides, es)
+        d[...] = s
+
+    def permute(self, src, shape, perm, es, dst):
+        a = _np(src).view(np.dtype((np.void, es))).reshape(tuple(shape))
+        out = _np(dst).view(np.dtype((np.void, es)))
+        out[...] = np.ascontiguousarray(a.transpose(perm)).reshape(-1)
+
+    def _planes(self, stat, code, x):
+        """x: (O, R, I) in the input dtype -> state planes (list of arrays (O*I,))."""
+        dt = np.dtype(_CODES[code])
+        if stat == STAT_SUM:
+            if dt == np.bool_:
+                return [x.any(axis=1).reshape(-1).astype(np.uint64)]
+            if dt.kind in 'iu':
+                return [np.add.reduce(x.astype(np.uint64), axis=1).reshape(-1)]
+            return [x.astype(np.float64).sum(axis=1).reshape(-1)]
+        v = x.astype(np.longdouble)
+        m = v.mean(axis=1)
+        m2 = ((v - m[:, None, :]) ** 2).sum(axis=1)
+        return [m.reshape(-1).astype(np.float64), m2.reshape(-1).astype(np.float64)]
+
+    def _finish(self, stat, code, planes, n, out, out_code):
+        dt = np.dtype(_CODES[code])
+        odt = np.dtype(_CODES[out_code])
+        o = _np(out).view(odt)
+        if stat == STAT_SUM:
+            if dt.kind in 'iub':
+                o[...] = planes[0].astype(dt) if dt != np.bool_ else planes[0] != 0
+            else:
+                o[...] = planes[0].astype(odt)
+            return
+        if stat == STAT_MEAN:
+            o[...] = planes[0].astype(odt)
+            return
+        var = planes[1] / n
+        o[...] = (var if stat == STAT_VAR else np.sqrt(var)).astype(odt)
+
+    def reduce(self, stat, src, code, O, R, I, out, out_code):
+        x = _np(src).view(_CODES[code]).reshape(O, R, I)
+        self._finish(stat, code, self._planes(stat, code, x), float(R), out, out_code)
+
+    def state_bytes(self, stat, code, nout):
+        mom = stat in (STAT_VAR, STAT_STD)
+        return (2 if mom else 1) * nout * 8
+
+    def reduce_state(self, stat, src, code, O, R, I, state):
+        x = _np(src).view(_CODES[code]).reshape(O, R, I)
+        planes = self._planes(stat, code, x)
+        buf = _np(state)
+        for i, p in enumerate(planes):
+            buf[i * O * I * 8:(i + 1) * O * I * 8] = p.view(np.uint8)
+        if stat == STAT_MEAN:
+            pass
+
+    def reduce_combine(self, stat, code, states, counts, nout, out, out_code):
+        buf = _np(states)
+        mom = stat in (STAT_VAR, STAT_STD)
+        npl = 2 if mom else 1
+        per = npl * nout * 8
+        dt = np.dtype(_CODES[code])
+        n, m, q = 0.0, np.zeros(nout), np.zeros(nout)
+        acc_u = np.zeros(nout, dtype=np.uint64)
+        acc_f = np.zeros(nout)
+        for p, c in enumerate(counts):
+            if c <= 0:
+                continue
+            part = buf[p * per:(p + 1) * per]
+            if stat == STAT_SUM:
+                if dt.kind in 'iub':
+                    u = part[:nout * 8].view(np.uint64)
+                    acc_u = (acc_u | u) if dt == np.bool_ else (acc_u + u)
+                else:
+                    acc_f = acc_f + part[:nout * 8].view(np.float64)
+                continue
+            mb = part[:nout * 8].view(np.float64)
+            qb = part[nout * 8:2 * nout * 8].view(np.float64) if mom else np.zeros(nout)
+            if n == 0:
+                n, m, q = float(c), mb.copy(), qb.copy()
+            else:
+                tot = n + c
+                d = mb - m
+                m = m + d * (c / tot)
+                q = q + qb + d * d * (n * c / tot)
+                n = tot
+        if stat == STAT_SUM:
+            planes = [acc_u] if dt.kind in 'iub' else [acc_f]
+        else:
+            planes = [m, q]
+        self._finish(stat, code, planes, n, out, out_code)
+
+
+def install():
+    from bolt_amd.mi355x._ops import register_backend
+    register_backend("cpu", CpuBackend())
+
+
+def uninstall():
+    from bolt_amd.mi355x._ops import register_backend
+    register_backend("cpu", None)

@@ -1,0 +1,87 @@
+"""Loader and comparison rules for the reference-generated golden fixtures.
+
+tests/golden/golden.json + golden.npz are written by tests/golden/make_golden.py
+from the reference bolt itself (Spark mode over an in-process RDD).  Inputs
+are regenerated from their specs (tests/golden/inputs.py).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+if GOLDEN not in sys.path:
+    sys.path.insert(0, GOLDEN)
+
+from inputs import make_input  # noqa: E402,F401
+
+_META = None
+_ARR = None
+
+
+def meta():
+    global _META, _ARR
+    if _META is None:
+        with open(os.path.join(GOLDEN, "golden.json")) as f:
+            _META = json.load(f)
+        _ARR = np.load(os.path.join(GOLDEN, "golden.npz"))
+    return _META
+
+
+def cases(op):
+    return [c for c in meta()["cases"] if c["op"] == op]
+
+
+def arr(case, name):
+    meta()
+    return _ARR["c%d_%s" % (case["id"], name)]
+
+
+def case_id(c):
+    return "c%d" % c["id"]
+
+
+def tup(v):
+    if v is None:
+        return None
+    if isinstance(v, list):
+        return tuple(v)
+    return v
+
+
+def size_arg(v):
+    return v if isinstance(v, str) else tup(v)
+
+
+def truth_stat(x, name, axis):
+    """float128 truth of a statistic (population var/std), kept axes ascending."""
+    ax = tuple(range(x.ndim)) if axis is None else (tuple(axis) if isinstance(axis, (list, tuple)) else (axis,))
+    v = x.astype(np.longdouble)
+    if name == "mean":
+        return v.mean(axis=ax)
+    if name == "sum":
+        return v.sum(axis=ax)
+    var = v.var(axis=ax)
+    return var if name == "var" else np.sqrt(var)
+
+
+def stat_close(got, ref, truth, out_dtype, x):
+    """The parity rule of SURVEY.md 8(c): |got-ref| <= rtol*|ref| + rtol*scale, with
+    rtol 1e-6 (float32/float16 outputs) / 1e-12 (float64); a result that is at least
+    as close to the float128 truth as the reference's also passes (the reference
+    accumulates float32 statistics in float32, order-dependently)."""
+    got = np.asarray(got, dtype=np.longdouble)
+    ref = np.asarray(ref, dtype=np.longdouble)
+    truth = np.asarray(truth, dtype=np.longdouble).reshape(ref.shape)
+    rtol = 1e-12 if np.dtype(out_dtype) == np.float64 else 1e-6
+    if np.dtype(out_dtype) == np.float16:
+        rtol = 1e-3
+    scale = max(float(np.max(np.abs(np.asarray(x, dtype=np.longdouble)))) if np.size(x) else 0.0,
+                float(np.max(np.abs(ref))) if ref.size else 0.0, 1e-300)
+    ok1 = np.abs(got - ref) <= rtol * np.abs(ref) + rtol * scale
+    eps = np.finfo(out_dtype).eps if np.dtype(out_dtype).kind == 'f' else 0
+    ok2 = np.abs(got - truth) <= np.abs(ref - truth) + 2 * eps * np.abs(truth) + eps * rtol * scale
+    both_nan = np.isnan(got) & np.isnan(ref)
+    return bool(np.all(ok1 | ok2 | both_nan))

@@ -1,4 +1,8 @@
-"""The reference's hot-path tests, run against the 'mi355x' mode on the GPU.
+"""The reference's hot-path tests, run against the 'mi355x' mode.
+
+Each test runs twice: on the GPU (marker `gpu`: the HIP kernels) and on the
+CPU test executor (tests/cpu_backend.py: the host logic -- plans, copy
+descriptors, formatting -- with numpy standing in for the kernels).
 
 Mirrors test/spark/test_spark_shaping.py:148-227 (swap, transpose, T,
 swapaxes), test/spark/test_spark_chunking.py:6-112 (chunk contents, unchunk,
@@ -15,36 +19,34 @@ import pytest
 import bolt_amd as bolt
 from bolt_amd.utils import allclose
 
-pytestmark = pytest.mark.gpu
-
 
 def exact(a, b):
     a, b = np.asarray(a), np.asarray(b)
     return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
 
 
-def test_construct(gpu_ctx):
+def test_construct(bctx):
     x = np.arange(2 * 3 * 4).reshape((2, 3, 4))
     for axis in [(0,), 0, (0, 1), (0, 1, 2)]:
-        b = bolt.array(x, gpu_ctx, axis=axis)
+        b = bolt.array(x, bctx, axis=axis)
         assert b.mode == 'mi355x'
         assert exact(b.toarray(), x)
     b = bolt.array(x, mode='mi355x')
     assert exact(b.toarray(), x)
     with pytest.raises(ValueError):
-        bolt.array(x, gpu_ctx, axis=-1)
+        bolt.array(x, bctx, axis=-1)
     with pytest.raises(ValueError):
-        bolt.array(x, gpu_ctx, axis=(0, 1, 2, 3))
+        bolt.array(x, bctx, axis=(0, 1, 2, 3))
     # non-leading key axes: the reference keeps the old shape (construct.py:48-67)
-    b = bolt.array(x, gpu_ctx, axis=(1,))
+    b = bolt.array(x, bctx, axis=(1,))
     assert exact(b.toarray(), x.transpose(1, 0, 2).reshape(x.shape))
-    assert exact(bolt.ones((2, 3, 4), gpu_ctx).toarray(), np.ones((2, 3, 4)))
-    assert exact(bolt.zeros(5, gpu_ctx, dtype=np.int16).toarray(), np.zeros(5, np.int16))
+    assert exact(bolt.ones((2, 3, 4), bctx).toarray(), np.ones((2, 3, 4)))
+    assert exact(bolt.zeros(5, bctx, dtype=np.int16).toarray(), np.zeros(5, np.int16))
 
 
-def test_swap(gpu_ctx):
+def test_swap(bctx):
     a = np.arange(2 ** 8).reshape(*(8 * [2]))
-    b = bolt.array(a, gpu_ctx, axis=(0, 1, 2, 3))
+    b = bolt.array(a, bctx, axis=(0, 1, 2, 3))
     bs = b.swap((1, 2), (0, 3), size=(2, 2))
     assert exact(bs.toarray(), a.transpose((0, 3, 4, 7, 1, 2, 5, 6)))
     bs = b.swap((1, 2), (0, 3), size="50")
@@ -58,26 +60,26 @@ def test_swap(gpu_ctx):
     assert exact(bs.toarray(), a) and bs.split == 5
     bs = b.swap(0, [])
     assert exact(bs.toarray(), a.transpose((1, 2, 3, 0, 4, 5, 6, 7))) and bs.split == 3
-    b = bolt.array(a, gpu_ctx, axis=range(8))
+    b = bolt.array(a, bctx, axis=range(8))
     bs = b.swap([0, 1], [])
     assert exact(bs.toarray(), a.transpose((2, 3, 4, 5, 6, 7, 0, 1))) and bs.split == 6
     a = np.arange(2 * 3 * 4).reshape(2, 3, 4)
-    b = bolt.array(a, gpu_ctx, axis=(0,))
+    b = bolt.array(a, bctx, axis=(0,))
     bs = b.swap((0,), (0, 1))
     assert exact(bs.toarray(), a.transpose(1, 2, 0))
     with pytest.raises(ValueError):
         b.swap((0,), ())
 
 
-def test_transpose_all_perms(gpu_ctx):
+def test_transpose_all_perms(bctx):
     a = np.arange(2 * 3 * 4 * 5).reshape((2, 3, 4, 5))
-    b = bolt.array(a, gpu_ctx, axis=(0, 1))
+    b = bolt.array(a, bctx, axis=(0, 1))
     for p in permutations(range(4), 4):
         t = b.transpose(p)
         assert exact(t.toarray(), a.transpose(p))
         assert t.split == 2
     assert exact(b.transpose().toarray(), a.transpose())
-    assert exact(bolt.array(a, gpu_ctx, axis=0).T.toarray(), a.T)
+    assert exact(bolt.array(a, bctx, axis=0).T.toarray(), a.T)
     assert exact(b.T.toarray(), a.T)
     for i, j in [(1, 2), (0, 1), (2, 3)]:
         assert exact(b.swapaxes(i, j).toarray(), a.swapaxes(i, j))
@@ -85,26 +87,26 @@ def test_transpose_all_perms(gpu_ctx):
         b.transpose((0, 1, 1, 2))
 
 
-def test_keys_values_transpose(gpu_ctx):
+def test_keys_values_transpose(bctx):
     x = np.arange(2 * 3 * 4).reshape((2, 3, 4))
-    b = bolt.array(x, gpu_ctx, axis=(0, 1))
+    b = bolt.array(x, bctx, axis=(0, 1))
     c = b.keys.transpose((1, 0))
     assert c.keys.shape == (3, 2)
     assert exact(c.toarray(), x.transpose((1, 0, 2)))
-    b = bolt.array(x, gpu_ctx, axis=0)
+    b = bolt.array(x, bctx, axis=0)
     c = b.values.transpose((1, 0))
     assert c.values.shape == (4, 3)
     assert exact(c.toarray(), x.transpose((0, 2, 1)))
     with pytest.raises(ValueError):
         b.values.transpose((0, 2))
-    b = bolt.array(x, gpu_ctx, axis=(0, 1))
+    b = bolt.array(x, bctx, axis=(0, 1))
     assert exact(b.keys.reshape((6,)).toarray(), x.reshape(6, 4))
     assert b.keys.reshape((6,)).split == 1
 
 
-def test_chunk_records(gpu_ctx):
+def test_chunk_records(bctx):
     x = np.arange(4 * 6).reshape(1, 4, 6)
-    b = bolt.array(x, gpu_ctx)
+    b = bolt.array(x, bctx)
     k1, v1 = zip(*b.chunk((2, 3))._rdd.sortByKey().collect())
     assert k1 == ((0, 0, 0), (0, 0, 1), (0, 1, 0), (0, 1, 1))
     v2 = [s for m in np.split(x[0], (2,), axis=0) for s in np.split(m, (3,), axis=1)]
@@ -114,23 +116,23 @@ def test_chunk_records(gpu_ctx):
     assert all(exact(m1, m2) for m1, m2 in zip(v1, v2))
 
 
-def test_unchunk(gpu_ctx):
+def test_unchunk(bctx):
     x = np.arange(4 * 6).reshape(1, 4, 6)
-    b = bolt.array(x, gpu_ctx)
+    b = bolt.array(x, bctx)
     for s in [(2, 3), (3, 4), (4, 6), '0.1', '150']:
         assert exact(b.chunk(s).unchunk().toarray(), x)
     x = np.arange(4 * 5 * 10).reshape(1, 4, 5, 10)
-    b = bolt.array(x, gpu_ctx)
+    b = bolt.array(x, bctx)
     for s in [(4, 5, 10), (1, 1, 1), (3, 3, 3)]:
         assert exact(b.chunk(s).unchunk().toarray(), x)
     x = np.arange(4 * 6).reshape(4, 6)
-    assert exact(bolt.array(x, gpu_ctx, (0, 1)).chunk(()).unchunk().toarray(), x)
-    assert exact(bolt.array(x, gpu_ctx, (0,)).chunk((2)).unchunk().toarray(), x)
+    assert exact(bolt.array(x, bctx, (0, 1)).chunk(()).unchunk().toarray(), x)
+    assert exact(bolt.array(x, bctx, (0,)).chunk((2)).unchunk().toarray(), x)
 
 
-def test_keys_to_values(gpu_ctx):
+def test_keys_to_values(bctx):
     x = np.arange(4 * 7 * 9 * 6).reshape(4, 7, 9, 6)
-    b = bolt.array(x, gpu_ctx, (0, 1))
+    b = bolt.array(x, bctx, (0, 1))
     c = b.chunk((4, 2))
     assert exact(x, c.keys_to_values((0,)).unchunk().toarray().transpose(1, 0, 2, 3))
     assert exact(x, c.keys_to_values((1,)).unchunk().toarray())
@@ -138,32 +140,32 @@ def test_keys_to_values(gpu_ctx):
     assert exact(x, c.keys_to_values((0, 1)).unchunk().toarray())
     assert exact(x, c.keys_to_values((0, 1), size=(2, 3)).unchunk().toarray())
     assert exact(x, c.keys_to_values(()).unchunk().toarray())
-    b = bolt.array(x, gpu_ctx, range(4))
+    b = bolt.array(x, bctx, range(4))
     c = b.chunk(())
     assert exact(x, c.keys_to_values((3,)).unchunk().toarray())
     assert exact(x, c.keys_to_values((0, 1)).unchunk().toarray().transpose(2, 3, 0, 1))
-    b = bolt.array(x, gpu_ctx, (0,))
+    b = bolt.array(x, bctx, (0,))
     c = b.chunk((2, 3, 4))
     assert exact(x, c.keys_to_values((0,)).unchunk().toarray())
 
 
-def test_values_to_keys(gpu_ctx):
+def test_values_to_keys(bctx):
     x = np.arange(4 * 7 * 9 * 6).reshape(4, 7, 9, 6)
-    b = bolt.array(x, gpu_ctx, (0, 1))
+    b = bolt.array(x, bctx, (0, 1))
     c = b.chunk((4, 2))
     assert exact(x, c.values_to_keys((0,)).unchunk().toarray())
     assert exact(x, c.values_to_keys((1,)).unchunk().toarray().transpose(0, 1, 3, 2))
     assert exact(x, c.values_to_keys((0, 1)).unchunk().toarray())
     assert exact(x, c.values_to_keys(()).unchunk().toarray())
-    b = bolt.array(x, gpu_ctx, (0,))
+    b = bolt.array(x, bctx, (0,))
     c = b.chunk((2, 3, 4))
     assert exact(x, c.values_to_keys((0,)).unchunk().toarray())
     assert exact(x, c.values_to_keys((0, 1)).unchunk().toarray())
 
 
-def test_padding(gpu_ctx):
+def test_padding(bctx):
     x = np.arange(2 * 2 * 5 * 6).reshape(2, 2, 5, 6)
-    b = bolt.array(x, gpu_ctx, (0, 1))
+    b = bolt.array(x, bctx, (0, 1))
     c = b.chunk((2, 2), padding=1)
     chunks = c.tordd().sortByKey().values().collect()
     assert exact(chunks[0], np.array([[0, 1, 2], [6, 7, 8], [12, 13, 14]]))
@@ -183,9 +185,9 @@ def test_padding(gpu_ctx):
         b.chunk((4, 4), padding=(2, 2))
 
 
-def test_chunk_properties(gpu_ctx):
+def test_chunk_properties(bctx):
     x = np.arange(4 * 6).reshape(1, 4, 6)
-    b = bolt.array(x, gpu_ctx)
+    b = bolt.array(x, bctx)
     assert b.chunk(size=(2, 3)).uniform is True
     assert b.chunk(size=(2, 4)).uniform is False
     with pytest.raises(ValueError):
@@ -193,9 +195,9 @@ def test_chunk_properties(gpu_ctx):
 
 
 @pytest.mark.parametrize("name", ["mean", "std", "var", "sum"])
-def test_stats(gpu_ctx, name):
+def test_stats(bctx, name):
     x = np.arange(2 * 3 * 4).reshape(2, 3, 4)
-    b = bolt.array(x, gpu_ctx, axis=(0,))
+    b = bolt.array(x, bctx, axis=(0,))
     f = getattr(b, name)
     g = getattr(x, name)
     assert allclose(f(), g())
@@ -207,17 +209,17 @@ def test_stats(gpu_ctx, name):
     assert f(axis=1, keepdims=True).shape == (2, 1, 4)
 
 
-def test_stats_dtypes(gpu_ctx):
+def test_stats_dtypes(bctx):
     rng = np.random.default_rng(0)
     x = (1000 + 50 * rng.standard_normal((200, 16, 8))).astype(np.float32)
-    b = bolt.array(x, gpu_ctx)
+    b = bolt.array(x, bctx)
     m = b.mean(axis=0)
     assert m.dtype == np.float32 and m.shape == (16, 8)
     assert np.allclose(m, x.astype(np.float64).mean(0), rtol=1e-6)
     s = b.std(axis=0)
     assert np.allclose(s, x.astype(np.float64).std(0), rtol=1e-5)
     u = rng.integers(0, 65536, size=(50, 8, 8)).astype(np.uint16)
-    bu = bolt.array(u, gpu_ctx)
+    bu = bolt.array(u, bctx)
     v = bu.var(axis=0)
     assert v.dtype == np.float64
     assert np.allclose(v, u.astype(np.float64).var(0), rtol=1e-12)

@@ -1,0 +1,144 @@
+"""Pin the CPU oracle (oracle/bolt_oracle.py) against the reference's own outputs.
+
+Every fixture in tests/golden was produced by the reference bolt (Spark mode,
+tests/golden/make_golden.py).  Data movement must match bit for bit (bytes,
+shape, split, chunk keys, plan, padding); statistics by the rule in
+golden_cases.stat_close; errors by exception type.
+"""
+import numpy as np
+import pytest
+
+import golden_cases as G
+from oracle import bolt_oracle as O
+
+
+def _rs(case, npart=2):
+    x = G.make_input(case["input"])
+    return x, O.parallelize(x, axis=G.tup(case["axis"]), npartitions=npart or 2)
+
+
+@pytest.mark.parametrize("case", G.cases("construct"), ids=G.case_id)
+def test_construct(case):
+    x = G.make_input(case["input"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.parallelize(x, axis=G.tup(case["axis"]))
+        assert type(e.value).__name__ == case["raises"]
+        return
+    rs = O.parallelize(x, axis=G.tup(case["axis"]), npartitions=case["npartitions"] or 2)
+    assert list(rs.shape) == case["shape"] and rs.split == case["split"]
+    assert O.toarray(rs).tobytes() == G.arr(case, "out").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("swap"), ids=G.case_id)
+def test_swap(case):
+    x, rs = _rs(case)
+    size = G.size_arg(case["size"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.swap(rs, G.tup(case["kaxes"]), G.tup(case["vaxes"]), size)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    out = O.swap(rs, G.tup(case["kaxes"]), G.tup(case["vaxes"]), size)
+    assert list(out.shape) == case["shape"] and out.split == case["split"]
+    got = O.toarray(out)
+    # key order (the reference's sortByKey order; see make_golden.py on toarray_unsorted)
+    want = G.arr(case, "out_sorted" if case.get("toarray_unsorted") else "out")
+    assert got.dtype == want.dtype and got.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("case", [c for c in G.cases("transpose") if "raises" not in c], ids=G.case_id)
+def test_transpose(case):
+    x, rs = _rs(case)
+    out = O.transpose(rs, case["perm"])
+    assert list(out.shape) == case["shape"] and out.split == case["split"]
+    assert O.toarray(out).tobytes() == G.arr(case, "out").tobytes()
+
+
+def _chunk_check(c, case):
+    recs = sorted(c.records(), key=lambda kv: kv[0])
+    assert [list(k) for k, _ in recs] == case["keys"]
+    assert [list(v.shape) for _, v in recs] == case["shapes"]
+    flat = np.concatenate([v.reshape(-1) for _, v in recs])
+    assert flat.tobytes() == G.arr(case, "flat").tobytes()
+    assert [int(p) for p in c.plan] == case["plan"]
+    assert [int(p) for p in c.padding] == case["padding_out"]
+
+
+@pytest.mark.parametrize("case", G.cases("chunk"), ids=G.case_id)
+def test_chunk(case):
+    x, rs = _rs(case)
+    size = case["size"]
+    size = size if isinstance(size, (str, int)) else tuple(size)
+    pad = G.tup(case["padding"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.chunk(rs, size, G.tup(case["chunk_axis"]), pad)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    c = O.chunk(rs, size, G.tup(case["chunk_axis"]), pad)
+    _chunk_check(c, case)
+    if "unchunk_raises" in case:
+        return
+    u = O.unchunk(c)
+    assert list(u.shape) == case["unchunk_shape"]
+    assert O.toarray(u).tobytes() == G.arr(case, "unchunk").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("moves"), ids=G.case_id)
+def test_moves(case):
+    x, rs = _rs(case)
+    size = case["size"]
+    size = size if isinstance(size, (str, int)) or size is None else tuple(size)
+    c = O.chunk(rs, size, None, G.tup(case["padding"]))
+
+    def apply(c):
+        for name, axes, z in case["steps"]:
+            c = O.keys_to_values(c, tuple(axes), size=G.tup(z)) if name == "k2v" else O.values_to_keys(c, tuple(axes))
+        return c
+    if "raises" in case:
+        with pytest.raises(Exception):
+            apply(c)
+        return
+    c = apply(c)
+    assert list(c.shape) == case["chunk_shape"] and c.split == case["split"]
+    _chunk_check(c, case)
+    u = O.unchunk(c)
+    assert O.toarray(u).tobytes() == G.arr(case, "unchunk").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("getplan"), ids=G.case_id)
+def test_getplan(case):
+    plan, pad = O.getplan(case["vshape"], case["dtype"], case["size"])
+    assert [int(p) for p in plan] == case["plan"]
+
+
+def _light(case):
+    # the C1 (100,64,64) inputs: keep the oracle run to a few seconds per case
+    if case["input"]["shape"] == [100, 64, 64]:
+        return case["reduce_axis"] in (0, [1, 2]) and not case["keepdims"]
+    return True
+
+
+@pytest.mark.parametrize("case", [c for c in G.cases("stat") if _light(c)], ids=G.case_id)
+def test_stat(case):
+    x = G.make_input(case["input"])
+    rs = O.parallelize(x, axis=G.tup(case["axis"]), npartitions=case["npartitions"] or 2)
+    name = {"var": "variance", "std": "stdev"}.get(case["name"], case["name"])
+    ax = G.tup(case["reduce_axis"])
+    f = (lambda: O.sum_(rs, ax, case["keepdims"])) if name == "sum" else \
+        (lambda: O.stat(rs, name, ax, case["keepdims"]))
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            f()
+        assert type(e.value).__name__ == case["raises"]
+        return
+    got = f()
+    want = G.arr(case, "out")
+    assert str(np.asarray(got).dtype) == case["result_dtype"]
+    assert np.asarray(got).shape == want.shape
+    if want.dtype.kind in 'iub':
+        assert np.asarray(got).tobytes() == want.tobytes()
+    else:
+        truth = G.truth_stat(x, case["name"], ax)
+        assert G.stat_close(got, want, truth, want.dtype, x)
