@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(kThreads)
     if (MODE == M_MEAN || MODE == M_MOM) {
       if (r < r_hi) {
         T v[VEC];
-        vload<T, VEC>(base + r * d.I, v);
+        vload_nt<T, VEC>(base + r * d.I, v);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[k].first(to_f64(v[k]));
         r += nph;
@@ -190,10 +190,10 @@ __global__ void __launch_bounds__(kThreads)
     }
     for (; r + 3 * nph < r_hi; r += 4 * nph) {
       T v0[VEC], v1[VEC], v2[VEC], v3[VEC];
-      vload<T, VEC>(base + r * d.I, v0);
-      vload<T, VEC>(base + (r + nph) * d.I, v1);
-      vload<T, VEC>(base + (r + 2 * nph) * d.I, v2);
-      vload<T, VEC>(base + (r + 3 * nph) * d.I, v3);
+      vload_nt<T, VEC>(base + r * d.I, v0);
+      vload_nt<T, VEC>(base + (r + nph) * d.I, v1);
+      vload_nt<T, VEC>(base + (r + 2 * nph) * d.I, v2);
+      vload_nt<T, VEC>(base + (r + 3 * nph) * d.I, v3);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) {
@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(kThreads)
     }
     for (; r < r_hi; r += nph) {
       T v[VEC];
-      vload<T, VEC>(base + r * d.I, v);
+      vload_nt<T, VEC>(base + r * d.I, v);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc[k].add(to_f64(v[k]));
@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(kThreads)
   if ((MODE == M_MEAN || MODE == M_MOM) && j < r_hi) {
     if (j + VEC <= r_hi) {
       T v[VEC];
-      vload<T, VEC>(row + j, v);
+      vload_nt<T, VEC>(row + j, v);
       acc.first(to_f64(v[0]));
 #pragma unroll
       for (int k = 1; k < VEC; ++k) acc.add(to_f64(v[k]));
@@ -322,8 +322,8 @@ __global__ void __launch_bounds__(kThreads)
   }
   for (; j + VEC + stride <= r_hi; j += 2 * stride) {
     T v0[VEC], v1[VEC];
-    vload<T, VEC>(row + j, v0);
-    vload<T, VEC>(row + j + stride, v1);
+    vload_nt<T, VEC>(row + j, v0);
+    vload_nt<T, VEC>(row + j + stride, v1);
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v0[k]));
@@ -342,7 +342,7 @@ __global__ void __launch_bounds__(kThreads)
   for (; j < r_hi; j += stride) {
     if (j + VEC <= r_hi) {
       T v[VEC];
-      vload<T, VEC>(row + j, v);
+      vload_nt<T, VEC>(row + j, v);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[k]));

@@ -35,6 +35,10 @@ class ChunkedArrayMI355X(object):
         self._ordered = ordered
         self._ctx = context
         self._geom = ChunkGeometry(self.vshape, self._plan, self._padding)
+        # values_to_keys down to no value axes appends a (1,) value axis whose
+        # records carry no chunk id (chunk.py:335-345); chunk() of an all-key
+        # array appends one with chunk id 0 (chunk.py:113-118)
+        self._bare_singleton = False
 
     # ---------------------------------------------------------- properties
     @property
@@ -214,13 +218,17 @@ class ChunkedArrayMI355X(object):
                 [self._split + v for v in vs[~vmask]])
         dense = self._unpack()
         shape_before = self._shape
+        bare = False
         if len(newshape) == newsplit:
             newshape = newshape + (1,)
             newplan = np.array([1])
             newpadding = np.array([0])
             perm = perm + [len(perm)]
             shape_before = shape_before + (1,)
-        return self._rechunk(dense, perm, shape_before, newshape, newsplit, newplan, newpadding)
+            bare = True
+        res = self._rechunk(dense, perm, shape_before, newshape, newsplit, newplan, newpadding)
+        res._bare_singleton = bare
+        return res
 
     # ------------------------------------------------------------- records
     def records(self):
@@ -244,7 +252,8 @@ class ChunkedArrayMI355X(object):
                 off = g.chunk_offset(j)
                 cs = g.chunk_shape(j)
                 n = int(np.prod(cs, dtype=np.int64))
-                yield (tuple(int(k) for k in key) + tuple(int(c) for c in j),
+                chk = () if self._bare_singleton else tuple(int(c) for c in j)
+                yield (tuple(int(k) for k in key) + chk,
                        host[base + off: base + off + n].reshape(cs).copy())
 
     def tordd(self):

@@ -83,11 +83,11 @@ class CpuBackend(object):
     def reduce_state(self, stat, src, code, O, R, I, state):
         x = _np(src).view(_CODES[code]).reshape(O, R, I)
         planes = self._planes(stat, code, x)
+        if stat == STAT_MEAN:
+            planes = planes[:1]  # the mean state is one plane (M2 is not kept)
         buf = _np(state)
         for i, p in enumerate(planes):
             buf[i * O * I * 8:(i + 1) * O * I * 8] = p.view(np.uint8)
-        if stat == STAT_MEAN:
-            pass
 
     def reduce_combine(self, stat, code, states, counts, nout, out, out_code):
         buf = _np(states)

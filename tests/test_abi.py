@@ -1,0 +1,65 @@
+"""The C-ABI library loads and exports every entry point include/bolt_mi355x.h
+declares, with the documented argument checking (no GPU needed: these calls
+fail before touching a device)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "bolt_mi355x.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(bm_\w+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from bolt_amd.mi355x import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libbolt_mi355x.so is not built (run __graft_entry__.build())")
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    from bolt_amd.mi355x import _lib
+    names = header_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), n
+    assert sorted(_lib.SIGNATURES) == names  # the ctypes binding covers exactly the header
+
+
+def test_abi_version(lib):
+    from bolt_amd.mi355x import _lib
+    assert lib.bm_abi_version() == _lib.ABI_VERSION == 1
+
+
+def test_argument_errors(lib):
+    from bolt_amd.mi355x import _lib
+    rc = lib.bm_copy_strided(None, None, -1, None, None, None, 4, None)
+    assert rc == -1 and b"bad arguments" in lib.bm_last_error()
+    rc = lib.bm_permute(None, None, 2, _lib.i64_array([2, 3]), _lib.i32_array([0, 0]), 4, None)
+    assert rc == -1 and b"invalid permutation" in lib.bm_last_error()
+    n = ctypes.c_size_t(0)
+    assert lib.bm_reduce_workspace_bytes(0, 10, 1, 0, 5, ctypes.byref(n)) == -1
+    assert b"empty reduction" in lib.bm_last_error()
+    assert lib.bm_reduce(7, None, 10, 1, 1, 1, None, 10, None, 0, None) == -1
+    assert lib.bm_reduce_combine(0, 10, None, None, 65, 1, None, 10, None) == -1
+
+
+def test_workspace_and_state_sizes(lib):
+    n = ctypes.c_size_t(0)
+    # C2 mean over time on the key=time layout: [1][2000][262144] -> chunked over R
+    assert lib.bm_reduce_workspace_bytes(0, 10, 1, 2000, 262144, ctypes.byref(n)) == 0
+    assert n.value % (262144 * 8) == 0 and n.value > 0
+    # row reduction with many rows needs no chunking
+    assert lib.bm_reduce_workspace_bytes(2, 10, 262144, 2000, 1, ctypes.byref(n)) == 0
+    assert n.value == 0
+    assert lib.bm_reduce_state_bytes(1, 10, 100, ctypes.byref(n)) == 0 and n.value == 1600
+    assert lib.bm_reduce_state_bytes(0, 3, 100, ctypes.byref(n)) == 0 and n.value == 800
+    assert lib.bm_reduce_state_bytes(3, 3, 100, ctypes.byref(n)) == 0 and n.value == 800

@@ -1,0 +1,129 @@
+"""Multi-rank orchestration of the mi355x mode on CPU: world_size 2 (and 3) over
+gloo, with the numpy test executor (tests/cpu_backend.py) in place of the HIP
+kernels.  Covers the paths that exchange data between ranks: the swap's
+pack -> all_to_all -> unpack, statistics over the sharded axis (states,
+all_gather, ordered Chan combine), output gathers, re-slabbing, and ragged /
+empty shards.  The collectives are the same torch.distributed calls the GPU
+path makes over RCCL.
+"""
+import os
+import socket
+import traceback
+from itertools import permutations
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _exact(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
+
+
+def _body(rank, world):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here)]
+    import cpu_backend
+    import bolt_amd as bolt
+    from bolt_amd import MI355XContext
+    cpu_backend.install()
+    ctx = MI355XContext(device="cpu")
+    assert ctx.world_size == world and ctx.rank == rank
+
+    rng = np.random.default_rng(0)
+    # C2-like: key = time, swap to key = voxel, stats over time
+    x = (1000 + 50 * rng.standard_normal((7, 6, 5))).astype(np.float32)
+    b = bolt.array(x, ctx)
+    lo, hi = ctx.local_bounds(7)
+    assert b._data.numel() == (hi - lo) * 30 * 4
+    s = b.swap((0,), (0, 1))
+    assert s.shape == (6, 5, 7) and s.split == 2
+    assert _exact(s.toarray(), x.transpose(1, 2, 0))
+    m = s.mean(axis=2)
+    assert m.dtype == np.float32 and np.allclose(m, x.astype(np.float64).mean(0), rtol=1e-6)
+    assert np.allclose(s.std(axis=2), x.astype(np.float64).std(0), rtol=1e-5)
+    # statistics over the sharded axis
+    for name in ("mean", "var", "std", "sum"):
+        got = getattr(b, name)(axis=0)
+        want = getattr(x.astype(np.float64), name)(axis=0)
+        assert np.allclose(got, want, rtol=1e-5), name
+        got = getattr(b, name)()
+        assert np.allclose(got, getattr(x.astype(np.float64), name)(), rtol=1e-5), name
+        got = getattr(b, name)(axis=(0, 2), keepdims=True)
+        assert np.asarray(got).shape == (1, 6, 1)
+    u = rng.integers(0, 65536, size=(9, 4, 3)).astype(np.uint16)
+    bu = bolt.array(u, ctx)
+    assert _exact(np.asarray(bu.sum(axis=0)), np.add.reduce(u, axis=0, dtype=np.uint16))
+    assert np.allclose(bu.var(axis=0), u.astype(np.float64).var(0), rtol=1e-12)
+    assert bu.var(axis=0).dtype == np.float64
+
+    # every permutation of a 4-d array with split 2 (a2a whenever perm[0] != 0)
+    a = np.arange(5 * 3 * 4 * 2).reshape(5, 3, 4, 2).astype(np.int16)
+    ba = bolt.array(a, ctx, axis=(0, 1))
+    for p in permutations(range(4)):
+        assert _exact(ba.transpose(p).toarray(), a.transpose(p)), p
+    assert _exact(ba.keys.transpose((1, 0)).toarray(), a.transpose(1, 0, 2, 3))
+    assert _exact(ba.keys.reshape((15,)).toarray(), a.reshape(15, 4, 2))
+    assert _exact(ba.values.reshape((8,)).toarray(), a.reshape(5, 3, 8))
+
+    # chunked records stay on their rank; moving the sharded key axis exchanges
+    c = ba.chunk((3, 1), padding=(1, 0))
+    assert _exact(c.unchunk().toarray(), a)
+    recs = list(c.records())
+    assert len(recs) == 15 * 2 * 2
+    k2v = c.keys_to_values((0,))
+    assert _exact(k2v.unchunk().toarray(), a.transpose(1, 0, 2, 3))
+    v2k = c.values_to_keys((1,))
+    assert _exact(v2k.unchunk().toarray(), a.transpose(0, 1, 3, 2))
+
+    # fewer records than ranks: empty shards
+    t = np.arange(2 * 3).reshape(1, 2, 3).astype(np.float64)
+    bt = bolt.array(t, ctx)
+    assert _exact(bt.toarray(), t)
+    assert _exact(bt.swap((0,), (0,)).toarray(), t.transpose(1, 0, 2))
+    assert np.allclose(bt.mean(axis=0), t.mean(0)) and np.allclose(bt.std(), t.std())
+    assert _exact(bolt.ones((3, 4), ctx, dtype=np.int32).toarray(), np.ones((3, 4), np.int32))
+
+
+def _worker(rank, world, port, errq):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        _body(rank, world)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multirank_gloo(world):
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
+    assert all(p.exitcode == 0 for p in procs)
