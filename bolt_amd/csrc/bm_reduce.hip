@@ -320,23 +320,20 @@ __global__ void __launch_bounds__(kThreads)
     }
     j += stride;
   }
-  for (; j + VEC + stride <= r_hi; j += 2 * stride) {
-    T v0[VEC], v1[VEC];
-    vload_nt<T, VEC>(row + j, v0);
-    vload_nt<T, VEC>(row + j + stride, v1);
+  // four 16-B vectors in flight per lane (HBM latency cover at 8 waves/SIMD)
+  for (; j + VEC + 3 * stride <= r_hi; j += 4 * stride) {
+    T v[4][VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v0[k]));
-      else if (MODE == M_FSUM) fs += to_f64(v0[k]);
-      else if (MODE == M_ISUM) us += to_u64(v0[k]);
-      else us |= (uint64_t)(v0[k] != 0);
-    }
+    for (int u = 0; u < 4; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v1[k]));
-      else if (MODE == M_FSUM) fs += to_f64(v1[k]);
-      else if (MODE == M_ISUM) us += to_u64(v1[k]);
-      else us |= (uint64_t)(v1[k] != 0);
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[u][k]));
+        else if (MODE == M_FSUM) fs += to_f64(v[u][k]);
+        else if (MODE == M_ISUM) us += to_u64(v[u][k]);
+        else us |= (uint64_t)(v[u][k] != 0);
+      }
     }
   }
   for (; j < r_hi; j += stride) {

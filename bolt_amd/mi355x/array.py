@@ -16,18 +16,42 @@ Operations and what replaces the Spark machinery:
       per-rank states -> all_gather -> ordered Chan combine.
   toarray / tolocal: D2H (+ all_gather of the slabs).
 """
+import functools
+
 import numpy as np
 
 from bolt_amd.mi355x import _lib
 from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
 from bolt_amd.mi355x.context import contiguous_strides, local_shape
-from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, _empty
+from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, _empty, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
 from bolt_amd.utils import tupleize, argpack, inshape, istransposeable
 
 _STAT_CODES = {'mean': _lib.STAT_MEAN, 'variance': _lib.STAT_VAR, 'stdev': _lib.STAT_STD}
+
+
+@functools.lru_cache(maxsize=256)
+def _plan_ok(vshape, dtype, size):
+    try:
+        plan, pad = getplan(vshape, dtype, size, None, None)
+        check_plan(plan, pad, vshape)
+    except Exception as e:  # cache the failure too; re-raised below
+        return e
+    return None
+
+
+def _check_swap_plan(vshape, dtype, size):
+    """getplan + _chunk's checks for the swap's chunk size (chunk.py:120-129), cached."""
+    try:
+        err = _plan_ok(tuple(vshape), np.dtype(dtype), size)
+    except TypeError:  # unhashable size: validate uncached
+        plan, pad = getplan(vshape, dtype, size, None, None)
+        check_plan(plan, pad, vshape)
+        return
+    if err is not None:
+        raise type(err)(*err.args)
 
 
 class BoltArrayMI355X(BoltArray):
@@ -220,10 +244,8 @@ class BoltArrayMI355X(BoltArray):
             return self
 
         # the chunk plan the reference would build (errors surface the same way)
-        vshape = self._shape[self._split:]
         if not (self._split == self.ndim):
-            plan, pad = getplan(vshape, self._dtype, size, None, None)
-            check_plan(plan, pad, vshape)
+            _check_swap_plan(self._shape[self._split:], self._dtype, size)
         # axes index boolean masks in the reference (chunk.py:224, :293):
         # negative axes count from the end, out-of-range ones raise IndexError
         nv = self.ndim - self._split
@@ -305,8 +327,7 @@ class BoltArrayMI355X(BoltArray):
                 for lo, hi in ctx.bounds(self._shape[0]):
                     sizes.append(int(np.prod((hi - lo,) + out_shape[1:], dtype=np.int64)) * out_dtype.itemsize)
                 out = all_gather_bytes(ctx, out, sizes)
-            host = out.cpu().numpy().view(out_dtype).reshape(out_shape)
-            return host, out_dtype
+            return to_host(out, out_dtype, out_shape), out_dtype
 
         # the sharded axis is reduced: per-rank states, gathered and combined
         # in rank order (statcounter.py:67-99, deterministic here)
@@ -325,8 +346,7 @@ class BoltArrayMI355X(BoltArray):
         states = all_gather_bytes(ctx, state, [sbytes] * ctx.world_size)
         out = _empty(nout * out_dtype.itemsize, dev)
         be.reduce_combine(stat, code, states, counts, nout, out, ocode)
-        host = out.cpu().numpy().view(out_dtype).reshape(out_shape)
-        return host, out_dtype
+        return to_host(out, out_dtype, out_shape), out_dtype
 
     def _stat(self, axis=None, func=None, name=None, keepdims=False):
         """Statistic over ``axis`` (array.py:284-334); results are host arrays / scalars."""
@@ -400,8 +420,7 @@ class BoltArrayMI355X(BoltArray):
 
     def toarray(self):
         """The whole array on the host (array.py:1006-1014)."""
-        host = self._gathered_bytes().cpu().numpy()
-        return host.view(self._dtype).reshape(self._shape)
+        return to_host(self._gathered_bytes(), self._dtype, self._shape)
 
     def tolocal(self):
         """As a local bolt array (array.py:999-1004)."""

@@ -243,7 +243,8 @@ class ChunkedArrayMI355X(object):
             buf = all_gather_bytes(ctx, self._packed, sizes)
         else:
             buf = self._packed
-        host = buf.cpu().numpy().view(self._dtype)
+        from bolt_amd.mi355x.dist import to_host
+        host = to_host(buf, self._dtype, (buf.numel() // self._dtype.itemsize,))
         kshape = self._shape[:self._split]
         ids = g.chunk_ids()
         for i, key in enumerate(np.ndindex(*kshape)):

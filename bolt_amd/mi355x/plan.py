@@ -5,6 +5,7 @@ Everything here is integer/shape arithmetic that decides what the HIP kernels
 do; no data is touched.  Each function restates (not copies) the reference
 semantics it cites, including the quirks a drop-in must keep.
 """
+import functools
 from itertools import product
 
 import numpy as np
@@ -307,7 +308,17 @@ def transpose_split(p, split):
 # reductions  (bolt/spark/array.py:_align, _stat, reduce)
 # --------------------------------------------------------------------------
 
+@functools.lru_cache(maxsize=1024)
+def _reduce_layout(shape, axes):
+    return _reduce_layout_impl(shape, axes)
+
+
 def reduce_layout(shape, axes):
+    """Cached front of _reduce_layout_impl (host planning stays off the critical path)."""
+    return _reduce_layout(tuple(int(x) for x in shape), tuple(sorted(set(int(a) for a in axes))))
+
+
+def _reduce_layout_impl(shape, axes):
     """Kernel layout for reducing ``axes`` of a C-contiguous array.
 
     Returns (perm, O, R, I): if ``perm`` is None the array is read in place
@@ -345,6 +356,11 @@ def reduce_layout(shape, axes):
 
 
 def stat_dtype(dtype, rec_shape):
+    return _stat_dtype(np.dtype(dtype), tuple(int(x) for x in rec_shape))
+
+
+@functools.lru_cache(maxsize=256)
+def _stat_dtype(dtype, rec_shape):
     """Result dtype of a StatCounter statistic (statcounter.py:51-59).
 
     The counter starts at mu = 0.0 (a Python float) and every statistic is
