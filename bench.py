@@ -244,7 +244,7 @@ def main():
         line["roofline"]["xgmi"] = {"peak_GBps_per_rank": (G - 1) * XGMI_LINK_GBPS,
                                     "payload_bytes_per_rank": int(payload)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rows = args.cpu_sample_rows or 1000
+        rows = args.cpu_sample_rows or 2000
         line["cpu_baseline"] = cpu_baseline(args.config, shape, dtype, rows)
     if rank == 0:
         print(json.dumps(line), flush=True)
