@@ -27,7 +27,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kUnroll = 4;
-constexpr int kTile = 64;
+constexpr int kArea = 4096;  // transpose tile = TA x (kArea / TA) elements
 
 // ---------------------------------------------------------------- rowcopy --
 template <int VB>
@@ -72,14 +72,19 @@ struct TransDesc {
   Decomp batch;    // remaining dims
 };
 
-// VA / VB: elements per lane for the global load (along a) / store (along b).
-template <typename T, int VA, int VB>
+// TA: tile extent along a (TB = kArea / TA along b), chosen on the host to
+// fit the two extents (a 32-wide source axis gets 32 x 128 tiles, not half-
+// empty 64 x 64 ones).  VA / VB: elements per lane for the global load
+// (along a) / store (along b).
+template <typename T, int TA, int VA, int VB>
 __global__ void __launch_bounds__(kThreads)
     k_transpose(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
-  __shared__ T tile[kTile][kTile + 1];
-  constexpr int NVA = kTile / VA;
+  constexpr int TB = kArea / TA;
+  __shared__ T tile[TB][TA + 1];
+  constexpr int NVA = TA / VA;
   constexpr int RPA = kThreads / NVA;
-  constexpr int NVB = kTile / VB;
+  constexpr int NVB = TB / VB;
+  static_assert(RPA <= TB && kThreads / NVB <= TA, "tile too small for the thread layout");
   constexpr int RPB = kThreads / NVB;
   const int tx = threadIdx.x % NVA, ty = threadIdx.x / NVA;
   const int ux = threadIdx.x % NVB, uy = threadIdx.x / NVB;
@@ -95,13 +100,13 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t tb = rem - ta * d.ntB.d;
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
-    const int64_t a0 = (int64_t)ta * kTile, b0 = (int64_t)tb * kTile;
+    const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
 
     // load: lanes walk dim a (source-contiguous)
     const T *s = src + so + a0 + b0 * d.sb;
     const bool fullA = (a0 + ia + VA <= d.La);
 #pragma unroll
-    for (int it = 0; it < kTile / RPA; ++it) {
+    for (int it = 0; it < TB / RPA; ++it) {
       const int rb = ty + it * RPA;
       if (b0 + rb < d.Lb) {
         const T *p = s + ia + (int64_t)rb * d.sb;
@@ -123,7 +128,7 @@ __global__ void __launch_bounds__(kThreads)
     T *q = dst + dof + b0 + a0 * d.da;
     const bool fullB = (b0 + ib + VB <= d.Lb);
 #pragma unroll
-    for (int it = 0; it < kTile / RPB; ++it) {
+    for (int it = 0; it < TA / RPB; ++it) {
       const int ra = uy + it * RPB;
       if (a0 + ra < d.La) {
         T v[VB];
@@ -226,22 +231,50 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   return BM_OK;
 }
 
-template <typename T>
-int launch_transpose_t(const T *src, T *dst, const TransDesc &td, int va_vec, int vb_vec,
-                       hipStream_t st) {
+template <typename T, int TA>
+void launch_transpose_ta(const T *src, T *dst, const TransDesc &td, bool va_vec, bool vb_vec, int grid,
+                         hipStream_t st) {
   constexpr int W = 16 / (int)sizeof(T);
+  if (va_vec && vb_vec)
+    k_transpose<T, TA, W, W><<<grid, kThreads, 0, st>>>(src, dst, td);
+  else if (va_vec)
+    k_transpose<T, TA, W, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+  else if (vb_vec)
+    k_transpose<T, TA, 1, W><<<grid, kThreads, 0, st>>>(src, dst, td);
+  else
+    k_transpose<T, TA, 1, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+}
+
+template <typename T>
+int launch_transpose_t(const T *src, T *dst, const TransDesc &td, int ta, bool va_vec, bool vb_vec,
+                       hipStream_t st) {
   uint64_t g = td.ntiles;
   if (g > 0x7fffffffull) g = 0x7fffffffull;
   const int grid = (int)g;
-  if (va_vec && vb_vec)
-    k_transpose<T, W, W><<<grid, kThreads, 0, st>>>(src, dst, td);
-  else if (va_vec)
-    k_transpose<T, W, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
-  else if (vb_vec)
-    k_transpose<T, 1, W><<<grid, kThreads, 0, st>>>(src, dst, td);
-  else
-    k_transpose<T, 1, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+  switch (ta) {
+    case 16: launch_transpose_ta<T, 16>(src, dst, td, va_vec, vb_vec, grid, st); break;
+    case 32: launch_transpose_ta<T, 32>(src, dst, td, va_vec, vb_vec, grid, st); break;
+    case 128: launch_transpose_ta<T, 128>(src, dst, td, va_vec, vb_vec, grid, st); break;
+    case 256: launch_transpose_ta<T, 256>(src, dst, td, va_vec, vb_vec, grid, st); break;
+    default: launch_transpose_ta<T, 64>(src, dst, td, va_vec, vb_vec, grid, st); break;
+  }
   return BM_OK;
+}
+
+// Tile shape with the least padding waste for extents (La, Lb); ties keep 64x64.
+int pick_tile_a(int64_t La, int64_t Lb) {
+  const int cands[5] = {64, 32, 128, 16, 256};
+  int best = 64;
+  double best_w = 1e300;
+  for (int ta : cands) {
+    const int tb = kArea / ta;
+    const double w = (double)(((La + ta - 1) / ta) * ta) * (double)(((Lb + tb - 1) / tb) * tb);
+    if (w < best_w * 0.97) {  // a new shape must save >3% of the tile traffic
+      best_w = w;
+      best = ta;
+    }
+  }
+  return best;
 }
 
 int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, int a, int es,
@@ -259,8 +292,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
     return BM_E_ARG;
   }
-  const uint64_t ntA = (uint64_t)((td.La + kTile - 1) / kTile);
-  const uint64_t ntB = (uint64_t)((td.Lb + kTile - 1) / kTile);
+  const int TA = pick_tile_a(td.La, td.Lb);
+  const int TB = kArea / TA;
+  const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);
+  const uint64_t ntB = (uint64_t)((td.Lb + TB - 1) / TB);
   uint64_t nb = 1;
   for (const Dim &x : batch) nb *= (uint64_t)x.n;
   td.ntB = make_fastdiv(ntB);
@@ -274,10 +309,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     if (k != b && (dims[k].ds * es) % 16) vb = false;
   }
   switch (es) {
-    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, va, vb, st);
-    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, va, vb, st);
-    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, va, vb, st);
-    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, va, vb, st);
+    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, TA, va, vb, st);
+    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, TA, va, vb, st);
+    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, TA, va, vb, st);
+    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, TA, va, vb, st);
     default: break;
   }
   bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);

@@ -26,6 +26,10 @@
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef BM_ROWS_UNROLL
+#define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
+#endif
+constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
 
 enum Mode { M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4 };
 
@@ -320,13 +324,13 @@ __global__ void __launch_bounds__(kThreads)
     }
     j += stride;
   }
-  // four 16-B vectors in flight per lane (HBM latency cover at 8 waves/SIMD)
-  for (; j + VEC + 3 * stride <= r_hi; j += 4 * stride) {
-    T v[4][VEC];
+  // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
+  for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
+    T v[kRowsUnroll][VEC];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
+    for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kRowsUnroll; ++u) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[u][k]));

@@ -42,6 +42,48 @@ def to_host(t, dtype, shape):
     return host.numpy().view(dtype).reshape(shape)
 
 
+# Optional phase timing of the exchange (bench.py sets it to a dict):
+# name -> list of (start, end) torch.cuda.Event pairs on the current stream.
+PROFILE = None
+
+
+class _phase(object):
+    def __init__(self, name, device):
+        self.name, self.device = name, device
+
+    def __enter__(self):
+        if PROFILE is not None and self.device.type == "cuda":
+            import torch
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+        return self
+
+    def __exit__(self, *exc):
+        if PROFILE is not None and self.device.type == "cuda":
+            self.ev[1].record()
+            PROFILE.setdefault(self.name, []).append(self.ev)
+        return False
+
+
+def _wide(t, sizes, unit):
+    """View a byte tensor as elements of ``unit`` bytes (1/2/4/8) so RCCL counts
+    stay small for multi-GB exchanges.  ``unit`` must be the same on every rank
+    (it is derived from global quantities: the element size, the row size)."""
+    import torch
+    if unit not in (4, 8):  # (gloo has no 16-bit collectives)
+        unit = 1
+    dt = {8: torch.int64, 4: torch.int32, 1: torch.uint8}[unit]
+    return t.view(dt), [int(s) // unit for s in sizes]
+
+
+def _unit(nbytes):
+    """Largest power of two <= 8 dividing ``nbytes`` (a global quantity)."""
+    u = 8
+    while u > 1 and int(nbytes) % u:
+        u //= 2
+    return u
+
+
 def all_gather_bytes(ctx, local, sizes):
     """Concatenate every rank's byte tensor (sizes[r] bytes from rank r) on every rank."""
     import torch
@@ -49,19 +91,25 @@ def all_gather_bytes(ctx, local, sizes):
     if ctx.world_size == 1:
         return local
     m = max(sizes) if sizes else 0
+    m = (m + 7) // 8 * 8
     buf = _empty(m, local.device)
     if local.numel():
         buf[:local.numel()].copy_(local)
     outs = [_empty(m, local.device) for _ in range(ctx.world_size)]
-    dist.all_gather(outs, buf, group=ctx.group)
+    wb, _ = _wide(buf, [m], 8)
+    wo = [_wide(o, [m], 8)[0] for o in outs]
+    dist.all_gather(wo, wb, group=ctx.group)
     return torch.cat([o[:s] for o, s in zip(outs, sizes)]) if m else _empty(0, local.device)
 
 
-def all_to_all_bytes(ctx, send, send_sizes, recv_sizes):
+def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1):
+    """Variable-size all-to-all of byte blocks; every size is a multiple of ``unit``."""
     import torch.distributed as dist
     recv = _empty(sum(recv_sizes), send.device)
-    dist.all_to_all_single(recv, send, output_split_sizes=[int(s) for s in recv_sizes],
-                           input_split_sizes=[int(s) for s in send_sizes], group=ctx.group)
+    ws, ss = _wide(send, send_sizes, unit)
+    wr, rs = _wide(recv, recv_sizes, unit)
+    with _phase("all_to_all", send.device):
+        dist.all_to_all_single(wr, ws, output_split_sizes=rs, input_split_sizes=ss, group=ctx.group)
     return recv
 
 
@@ -101,12 +149,13 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
     send_sizes = [int(np.prod(b)) * es for _, b in blocks]
     send = _empty(sum(send_sizes), data.device)
     off = 0
-    for (qlo, bshape), nb in zip(blocks, send_sizes):
-        if nb:
-            sstr = [sin[p] for p in perm]
-            backend.copy_strided(data, qlo * sin[a] * es, send, off, bshape, sstr,
-                                 contiguous_strides(bshape), es)
-        off += nb
+    with _phase("pack", data.device):
+        for (qlo, bshape), nb in zip(blocks, send_sizes):
+            if nb:
+                sstr = [sin[p] for p in perm]
+                backend.copy_strided(data, qlo * sin[a] * es, send, off, bshape, sstr,
+                                     contiguous_strides(bshape), es)
+            off += nb
 
     lo, hi = out_b[r]
     loc_out = (hi - lo,) + out_shape[1:]
@@ -118,16 +167,17 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
         bshape[j] = shi - slo
         rblocks.append((slo, bshape))
         recv_sizes.append(int(np.prod(bshape)) * es)
-    recv = all_to_all_bytes(ctx, send, send_sizes, recv_sizes)
+    recv = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(es))
 
     out = _empty(int(np.prod(loc_out)) * es, data.device)
     tstr = contiguous_strides(loc_out)
     off = 0
-    for (slo, bshape), nb in zip(rblocks, recv_sizes):
-        if nb:
-            backend.copy_strided(recv, off, out, slo * tstr[j] * es, bshape,
-                                 contiguous_strides(bshape), tstr, es)
-        off += nb
+    with _phase("unpack", data.device):
+        for (slo, bshape), nb in zip(rblocks, recv_sizes):
+            if nb:
+                backend.copy_strided(recv, off, out, slo * tstr[j] * es, bshape,
+                                     contiguous_strides(bshape), tstr, es)
+            off += nb
     return out
 
 
@@ -146,4 +196,4 @@ def redistribute_rows(ctx, data, old_rows, old_rowbytes, new_rows, new_rowbytes)
     send_sizes = [max(0, min(mhi, qhi) - max(mlo, qlo)) for qlo, qhi in nb]
     tlo, thi = nb[r]
     recv_sizes = [max(0, min(thi, shi) - max(tlo, slo)) for slo, shi in ob]
-    return all_to_all_bytes(ctx, data, send_sizes, recv_sizes)
+    return all_to_all_bytes(ctx, data, send_sizes, recv_sizes, _unit(np.gcd(old_rowbytes, new_rowbytes)))

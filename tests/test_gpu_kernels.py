@@ -60,6 +60,13 @@ def test_permute_all_perms_4d(dtype):
     ((3, 4, 5, 6, 7), (4, 3, 2, 1, 0)),
     ((4, 6, 8, 10, 3), (2, 0, 4, 1, 3)),
     ((2,) * 8, (0, 3, 4, 7, 1, 2, 5, 6)),
+    # tile-shape selection (La = source-contiguous extent, Lb = destination-contiguous)
+    ((3000, 16), (1, 0)),        # La 16   -> 16 x 256 tiles
+    ((16, 3000), (1, 0)),        # Lb 16   -> 256 x 16 tiles
+    ((700, 32), (1, 0)),         # La 32   -> 32 x 128 tiles
+    ((40, 300, 32), (2, 1, 0)),  # C3 .T shape family
+    ((33, 130, 9), (2, 1, 0)),
+    ((2, 8, 300), (2, 0, 1)),
 ])
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64])
 def test_permute_shapes(shape, perm, dtype):

@@ -1,0 +1,129 @@
+"""Interleaved A/B timing of libbolt_mi355x builds on the BASELINE shapes.
+
+    python tools/ab_bench.py libA.so [libB.so ...] [--ops c2_swap,c2_mean_rows,...] [--rounds 5]
+
+Every library is loaded side by side in ONE process and the variants run in
+interleaved rounds on the same buffers (cdna_hip_programming.md §5.4 rule 24);
+each op reports the median kernel time (hipEvents) and GB/s of algorithmic
+bytes.  Build variants with  make -C bolt_amd/csrc OUT=/tmp/x.so BUILD=/tmp/bx EXTRA=-D...
+"""
+import argparse
+import ctypes
+import sys
+
+import numpy as np
+import torch
+
+I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    lib.bm_permute.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, I64P,
+                               ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_void_p]
+    lib.bm_copy_strided.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, I64P, I64P, I64P,
+                                    ctypes.c_int, ctypes.c_void_p]
+    lib.bm_reduce.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                              ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_size_t, ctypes.c_void_p]
+    lib.bm_reduce_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                              ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]
+    lib.bm_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def i64(v):
+    return (ctypes.c_int64 * len(v))(*[int(x) for x in v])
+
+
+def i32(v):
+    return (ctypes.c_int32 * len(v))(*[int(x) for x in v])
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Permute(object):
+    def __init__(self, shape, perm, dtype):
+        self.shape, self.perm, self.es = shape, perm, np.dtype(dtype).itemsize
+        n = int(np.prod(shape)) * self.es
+        self.src = torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty_like(self.src)
+        self.bytes = 2 * n
+
+    def __call__(self, lib):
+        rc = lib.bm_permute(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
+                            len(self.shape), i64(self.shape), i32(self.perm), self.es, stream())
+        assert rc == 0, lib.bm_last_error()
+
+
+class Reduce(object):
+    CODES = {np.dtype(np.float32): 10, np.dtype(np.float64): 11, np.dtype(np.uint16): 3}
+
+    def __init__(self, stat, O, R, I, dtype, out_dtype):
+        self.stat, self.O, self.R, self.I = stat, O, R, I
+        self.code = self.CODES[np.dtype(dtype)]
+        self.ocode = self.CODES[np.dtype(out_dtype)]
+        n = O * R * I * np.dtype(dtype).itemsize
+        self.src = (torch.randn(n // 4, device="cuda") * 50 + 1000).view(torch.uint8) \
+            if np.dtype(dtype) == np.float32 else torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")
+        self.out = torch.empty(O * I * np.dtype(out_dtype).itemsize, dtype=torch.uint8, device="cuda")
+        self.ws = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
+        self.bytes = n + self.out.numel()
+
+    def __call__(self, lib):
+        rc = lib.bm_reduce(self.stat, ctypes.c_void_p(self.src.data_ptr()), self.code, self.O, self.R, self.I,
+                           ctypes.c_void_p(self.out.data_ptr()), self.ocode,
+                           ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(), stream())
+        assert rc == 0, lib.bm_last_error()
+
+
+OPS = {
+    "c2_swap": lambda: Permute((2000, 512 * 512), (1, 0), np.float32),
+    "c2_mean_rows": lambda: Reduce(0, 512 * 512, 2000, 1, np.float32, np.float32),
+    "c2_std_rows": lambda: Reduce(2, 512 * 512, 2000, 1, np.float32, np.float32),
+    "c2_mean_cols": lambda: Reduce(0, 1, 2000, 512 * 512, np.float32, np.float32),
+    "c2_std_cols": lambda: Reduce(2, 1, 2000, 512 * 512, np.float32, np.float32),
+    "c3_swap": lambda: Permute((1024, 256, 256, 32), (1, 2, 0, 3), np.float32),
+    "c3_T": lambda: Permute((1024, 256, 256, 32), (3, 2, 1, 0), np.float32),
+    "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
+    "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
+    "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),
+    "c5_perm": lambda: Permute((64, 64, 64, 64, 64), (2, 0, 4, 1, 3), np.float64),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--ops", default=",".join(OPS))
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    libs = [load(p) for p in a.libs]
+    for name in a.ops.split(","):
+        op = OPS[name]()
+        times = [[] for _ in libs]
+        for _ in range(2):
+            for lib in libs:
+                op(lib)
+        for _ in range(a.rounds):
+            for k, lib in enumerate(libs):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    op(lib)
+                e1.record()
+                e1.synchronize()
+                times[k].append(e0.elapsed_time(e1) / a.reps)
+        for k, p in enumerate(a.libs):
+            ms = float(np.median(times[k]))
+            print("%-14s %-40s %8.4f ms  %8.1f GB/s  (min %.4f)" % (name, p.split("/")[-1], ms,
+                  op.bytes / ms / 1e6, min(times[k])), flush=True)
+        del op
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    sys.exit(main())
