@@ -223,6 +223,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    from bolt_amd.mi355x import dist as bdist
+    if world > 1:
+        bdist.PROFILE = {}  # hipEvent pairs around pack / all_to_all / unpack
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -250,6 +253,11 @@ def main():
         del s, workload_swap
     barrier()
     elapsed = time.perf_counter() - t0
+    phases = {}
+    if bdist.PROFILE is not None:
+        for k, evs in bdist.PROFILE.items():
+            phases[k] = float(np.mean([a.elapsed_time(z) for a, z in evs]))
+        bdist.PROFILE = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -293,9 +301,25 @@ def main():
     }
     if world > 1:
         G = world
-        payload = per["swap"] / 2 * (G - 1) / G / G  # bytes each rank sends to peers
-        line["roofline"]["xgmi"] = {"peak_GBps_per_rank": (G - 1) * XGMI_LINK_GBPS,
-                                    "payload_bytes_per_rank": int(payload)}
+        n_rank = per["swap"] / 2 / G                  # bytes held per rank
+        payload = n_rank * (G - 1) / G                # bytes each rank sends to its peers
+        ex = phases.get("exchange")
+        if ex:  # the swap across GPUs: pipelined pack -> RCCL all-to-all -> unpack
+            line["roofline"].update({"kernel": "swap exchange per rank (k_transpose pack + RCCL "
+                                               "all_to_all + k_rowcopy unpack, pipelined)",
+                                     "achieved": round(2 * n_rank / (ex / 1e3) / 1e9, 1),
+                                     "avg_ms": round(ex, 4), "bytes_per_launch": int(2 * n_rank)})
+            line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
+        a2a = phases.get("exchange")
+        peak = (G - 1) * XGMI_LINK_GBPS
+        line["xgmi"] = {"op": "RCCL all_to_all_single inside the pipelined swap exchange "
+                              "(achieved = peer payload / whole exchange time: a lower bound)",
+                        "payload_bytes_per_rank": int(payload),
+                        "avg_ms": round(a2a, 4) if a2a else None,
+                        "achieved": round(payload / (a2a / 1e3) / 1e9, 1) if a2a else None,
+                        "peak": peak, "unit": "GB/s per rank (egress)",
+                        "frac": round(payload / (a2a / 1e3) / 1e9 / peak, 4) if a2a else None,
+                        "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
     if rank == 0 and world == 1 and not args.no_pmc:
         traffic, note = pmc_traffic(args.config)
         line["roofline"]["traffic"] = int(traffic) if traffic else None

@@ -42,6 +42,10 @@ def to_host(t, dtype, shape):
     return host.numpy().view(dtype).reshape(shape)
 
 
+# Pipeline depth of the swap exchange (None: from the message size, >= 32 MiB
+# per peer per stage, at most 8 stages); tests set it to exercise the stages.
+STAGES = None
+
 # Optional phase timing of the exchange (bench.py sets it to a dict):
 # name -> list of (start, end) torch.cuda.Event pairs on the current stream.
 PROFILE = None
@@ -84,12 +88,22 @@ def _unit(nbytes):
     return u
 
 
+def _host_staged(ctx, t):
+    """gloo cannot run these collectives on GPU tensors: stage them through the
+    host (used to rehearse the multi-rank GPU path on a single device; RCCL,
+    the production transport, moves device memory directly over xGMI)."""
+    import torch.distributed as dist
+    return t.device.type == "cuda" and dist.get_backend(ctx.group) == "gloo"
+
+
 def all_gather_bytes(ctx, local, sizes):
     """Concatenate every rank's byte tensor (sizes[r] bytes from rank r) on every rank."""
     import torch
     import torch.distributed as dist
     if ctx.world_size == 1:
         return local
+    if _host_staged(ctx, local):
+        return all_gather_bytes(ctx, local.cpu(), sizes).to(local.device)
     m = max(sizes) if sizes else 0
     m = (m + 7) // 8 * 8
     buf = _empty(m, local.device)
@@ -102,15 +116,22 @@ def all_gather_bytes(ctx, local, sizes):
     return torch.cat([o[:s] for o, s in zip(outs, sizes)]) if m else _empty(0, local.device)
 
 
-def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1):
-    """Variable-size all-to-all of byte blocks; every size is a multiple of ``unit``."""
+def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1, async_op=False):
+    """Variable-size all-to-all of byte blocks; every size is a multiple of ``unit``.
+
+    With async_op the call returns (recv, work): the exchange runs on the
+    collective's own stream and ``work.wait()`` orders the caller's stream
+    after it (no host block on RCCL)."""
     import torch.distributed as dist
+    if _host_staged(ctx, send):
+        recv = all_to_all_bytes(ctx, send.cpu(), send_sizes, recv_sizes, unit).to(send.device)
+        return (recv, None) if async_op else recv
     recv = _empty(sum(recv_sizes), send.device)
     ws, ss = _wide(send, send_sizes, unit)
     wr, rs = _wide(recv, recv_sizes, unit)
-    with _phase("all_to_all", send.device):
-        dist.all_to_all_single(wr, ws, output_split_sizes=rs, input_split_sizes=ss, group=ctx.group)
-    return recv
+    work = dist.all_to_all_single(wr, ws, output_split_sizes=rs, input_split_sizes=ss, group=ctx.group,
+                                  async_op=async_op)
+    return (recv, work) if async_op else recv
 
 
 def permute_sharded(ctx, backend, data, shape, perm, es):
@@ -139,46 +160,70 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
 
     a = perm[0]          # input axis that becomes the output's leading axis
     j = perm.index(0)    # where the input's leading axis lands
-    blocks = []
-    for q in range(ctx.world_size):
-        qlo, qhi = out_b[q]
-        bshape = list(out_shape)
-        bshape[0] = qhi - qlo
-        bshape[j] = in_hi - in_lo
-        blocks.append((qlo, bshape))
-    send_sizes = [int(np.prod(b)) * es for _, b in blocks]
-    send = _empty(sum(send_sizes), data.device)
-    off = 0
-    with _phase("pack", data.device):
-        for (qlo, bshape), nb in zip(blocks, send_sizes):
-            if nb:
-                sstr = [sin[p] for p in perm]
-                backend.copy_strided(data, qlo * sin[a] * es, send, off, bshape, sstr,
-                                     contiguous_strides(bshape), es)
-            off += nb
-
+    G = ctx.world_size
     lo, hi = out_b[r]
     loc_out = (hi - lo,) + out_shape[1:]
-    recv_sizes = []
-    rblocks = []
-    for s in range(ctx.world_size):
-        slo, shi = in_b[s]
-        bshape = list(loc_out)
-        bshape[j] = shi - slo
-        rblocks.append((slo, bshape))
-        recv_sizes.append(int(np.prod(bshape)) * es)
-    recv = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(es))
-
     out = _empty(int(np.prod(loc_out)) * es, data.device)
     tstr = contiguous_strides(loc_out)
-    off = 0
-    with _phase("unpack", data.device):
-        for (slo, bshape), nb in zip(rblocks, recv_sizes):
-            if nb:
-                backend.copy_strided(recv, off, out, slo * tstr[j] * es, bshape,
-                                     contiguous_strides(bshape), tstr, es)
-            off += nb
+    sstr = [sin[p] for p in perm]
+    # Pipeline the exchange in K stages along the output rows: stage k packs
+    # its sub-blocks, starts its all-to-all asynchronously (RCCL stream) and,
+    # while that runs, the current stream unpacks stage k-1 and packs k+1.
+    per_peer = (in_hi - in_lo) * int(np.prod(shape[1:])) * es // G
+    K = STAGES if STAGES else int(max(1, min(8, per_peer // (32 << 20))))
+    K = max(1, min(K, min(b - a_ for a_, b in out_b) or 1))
+
+    def sub(q, k):
+        qlo, qhi = out_b[q]
+        n = qhi - qlo
+        return qlo + k * n // K, qlo + (k + 1) * n // K
+
+    with _phase("exchange", data.device):
+        pending = None
+        for k in range(K):
+            send_sizes, parts = [], []
+            for q in range(G):
+                slo_q, shi_q = sub(q, k)
+                bshape = list(out_shape)
+                bshape[0] = shi_q - slo_q
+                bshape[j] = in_hi - in_lo
+                parts.append((slo_q, bshape))
+                send_sizes.append(int(np.prod(bshape)) * es)
+            send = _empty(sum(send_sizes), data.device)
+            off = 0
+            for (slo_q, bshape), nb in zip(parts, send_sizes):
+                if nb:
+                    backend.copy_strided(data, slo_q * sin[a] * es, send, off, bshape, sstr,
+                                         contiguous_strides(bshape), es)
+                off += nb
+            mlo, mhi = sub(r, k)
+            recv_sizes, rparts = [], []
+            for s_ in range(G):
+                slo, shi = in_b[s_]
+                bshape = list(loc_out)
+                bshape[0] = mhi - mlo
+                bshape[j] = shi - slo
+                rparts.append((slo, bshape))
+                recv_sizes.append(int(np.prod(bshape)) * es)
+            recv, work = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(es), async_op=True)
+            if pending is not None:
+                _unpack(backend, pending, out, tstr, j, es)
+            pending = (recv, work, send, rparts, recv_sizes, mlo - lo)
+        _unpack(backend, pending, out, tstr, j, es)
     return out
+
+
+def _unpack(backend, pending, out, tstr, j, es):
+    recv, work, send, rparts, recv_sizes, row0 = pending
+    if work is not None:
+        work.wait()  # the current stream waits for this stage's all-to-all
+    off = 0
+    for (slo, bshape), nb in zip(rparts, recv_sizes):
+        if nb:
+            backend.copy_strided(recv, off, out, (row0 * tstr[0] + slo * tstr[j]) * es, bshape,
+                                 contiguous_strides(bshape), tstr, es)
+        off += nb
+    del send
 
 
 def redistribute_rows(ctx, data, old_rows, old_rowbytes, new_rows, new_rowbytes):

@@ -29,15 +29,16 @@ def _exact(a, b):
     return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
 
 
-def _body(rank, world):
+def _body(rank, world, device="cpu"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.dirname(here)]
-    import cpu_backend
     import bolt_amd as bolt
     from bolt_amd import MI355XContext
-    cpu_backend.install()
-    ctx = MI355XContext(device="cpu")
+    if device == "cpu":
+        import cpu_backend
+        cpu_backend.install()
+    ctx = MI355XContext(device=device)
     assert ctx.world_size == world and ctx.rank == rank
 
     rng = np.random.default_rng(0)
@@ -67,11 +68,18 @@ def _body(rank, world):
     assert np.allclose(bu.var(axis=0), u.astype(np.float64).var(0), rtol=1e-12)
     assert bu.var(axis=0).dtype == np.float64
 
-    # every permutation of a 4-d array with split 2 (a2a whenever perm[0] != 0)
+    # every permutation of a 4-d array with split 2 (a2a whenever perm[0] != 0),
+    # with the exchange in 1 stage and pipelined over 2 and 3 stages
+    from bolt_amd.mi355x import dist as bdist
     a = np.arange(5 * 3 * 4 * 2).reshape(5, 3, 4, 2).astype(np.int16)
     ba = bolt.array(a, ctx, axis=(0, 1))
-    for p in permutations(range(4)):
-        assert _exact(ba.transpose(p).toarray(), a.transpose(p)), p
+    for stages in (None, 2, 3):
+        bdist.STAGES = stages
+        for p in permutations(range(4)):
+            assert _exact(ba.transpose(p).toarray(), a.transpose(p)), (p, stages)
+        y = (np.arange(11 * 7 * 6) % 251).astype(np.float32).reshape(11, 7, 6)
+        assert _exact(bolt.array(y, ctx).swap((0,), (0, 1)).toarray(), y.transpose(1, 2, 0))
+    bdist.STAGES = None
     assert _exact(ba.keys.transpose((1, 0)).toarray(), a.transpose(1, 0, 2, 3))
     assert _exact(ba.keys.reshape((15,)).toarray(), a.reshape(15, 4, 2))
     assert _exact(ba.values.reshape((8,)).toarray(), a.reshape(5, 3, 8))
@@ -95,13 +103,13 @@ def _body(rank, world):
     assert _exact(bolt.ones((3, 4), ctx, dtype=np.int32).toarray(), np.ones((3, 4), np.int32))
 
 
-def _worker(rank, world, port, errq):
+def _worker(rank, world, port, errq, device="cpu"):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        _body(rank, world)
+        _body(rank, world, device)
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
@@ -109,12 +117,11 @@ def _worker(rank, world, port, errq):
         raise
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_multirank_gloo(world):
+def _run(world, device):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, errq)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, errq, device)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -127,3 +134,18 @@ def test_multirank_gloo(world):
             p.kill()
     assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multirank_gloo(world):
+    _run(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_multirank_gpu_kernels_one_device():
+    """The same multi-rank flow with the HIP kernels: 2 ranks share cuda:0,
+    exchanges over gloo staged through the host (RCCL needs distinct GPUs)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(2, "cuda:0")
