@@ -26,23 +26,40 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 4;
+// rowcopy launch shape (A/B knobs, tools/ab_bench.py)
+#ifndef BM_RC_THREADS
+#define BM_RC_THREADS 256
+#endif
+#ifndef BM_RC_UNROLL
+#define BM_RC_UNROLL 1
+#endif
+#ifndef BM_RC_GRIDCAP
+#define BM_RC_GRIDCAP 262144  // A/B (profiles/r01_ab3/ab4): one vector per lane, many blocks: +8-15% on C3/C4 swaps
+#endif
+#ifndef BM_RUNS_T
+#define BM_RUNS_T 1
+#endif
+#ifndef BM_RUNS_MAXB
+#define BM_RUNS_MAXB 64  // runs of 128 B (C3) move as fast through rowcopy (profiles/r01_ab4)
+#endif
+constexpr int kRcThreads = BM_RC_THREADS;
+constexpr int kUnroll = BM_RC_UNROLL;
 constexpr int kArea = 4096;  // transpose tile = TA x (kArea / TA) elements
 
 // ---------------------------------------------------------------- rowcopy --
 template <int VB>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kRcThreads)
     k_rowcopy(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
               FastDiv vpr, uint64_t total, int es) {
   typedef typename VecB<VB>::t V;
-  const uint64_t step = (uint64_t)gridDim.x * kThreads * kUnroll;
-  for (uint64_t base = (uint64_t)blockIdx.x * kThreads * kUnroll + threadIdx.x;
+  const uint64_t step = (uint64_t)gridDim.x * kRcThreads * kUnroll;
+  for (uint64_t base = (uint64_t)blockIdx.x * kRcThreads * kUnroll + threadIdx.x;
        base < total; base += step) {
     V reg[kUnroll];
     int64_t doff[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const uint64_t g = base + (uint64_t)u * kThreads;
+      const uint64_t g = base + (uint64_t)u * kRcThreads;
       doff[u] = -1;
       if (g < total) {
         const uint64_t row = fd_div(g, vpr);
@@ -148,6 +165,73 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+
+// ------------------------------------------------------------ runs transpose --
+// A permutation that keeps a short innermost run (W 16-B units, 32-256 B) but
+// swaps the two axes around it (C3 / the 64 GiB target: swap((0,),(0,)) on
+// (K0, K1, V0, 32) float32) is a transpose of W-unit "super elements".  Moving
+// runs one by one reads 128-B pieces megabytes apart; tiling TA x TB runs
+// through LDS reads TA*W units (2 KiB) contiguously per source row and writes
+// TB*W units contiguously per destination row.
+struct RunsDesc {
+  int64_t La, Lb;    // extents of dims A (source-contiguous runs) and B (destination-contiguous runs)
+  int64_t sb;        // source stride of B, in 16-B units
+  int64_t da;        // destination stride of A, in 16-B units
+  FastDiv ntB;       // tiles along B
+  FastDiv ntAB;      // tiles per batch element
+  uint64_t ntiles;
+  Decomp batch;      // remaining dims (strides in 16-B units)
+};
+
+constexpr int kRunUnits = 128;  // units per tile row along A (2 KiB)
+constexpr int kRunTB = 16;      // tile rows along B
+
+template <int W>
+__global__ void __launch_bounds__(kThreads)
+    k_transpose_runs(const uint4 *__restrict__ src, uint4 *__restrict__ dst, RunsDesc d) {
+  constexpr int TA = kRunUnits / W;
+  constexpr int PAD = W < 16 ? W : 0;  // spreads 16-lane read groups over both bank halves
+  constexpr int ROW = kRunUnits + PAD;
+  __shared__ uint4 tile[kRunTB * ROW];
+  typedef typename VecB<16>::t V;
+  for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
+    const uint64_t bt = fd_div(t, d.ntAB);
+    const uint64_t rem = t - bt * d.ntAB.d;
+    const uint64_t ta = fd_div(rem, d.ntB);
+    const uint64_t tb = rem - ta * d.ntB.d;
+    int64_t so, dof;
+    decomp2(bt, d.batch, so, dof);
+    const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * kRunTB;
+    const int64_t na = min((int64_t)TA, d.La - a0);   // runs in this tile along A
+    const int64_t nb = min((int64_t)kRunTB, d.Lb - b0);
+    // load: source row b holds na*W contiguous units starting at run a0
+    const uint4 *s = src + so + a0 * W + b0 * d.sb;
+#pragma unroll
+    for (int it = 0; it < kRunTB * kRunUnits / kThreads; ++it) {
+      const int idx = it * kThreads + threadIdx.x;
+      const int rb = idx / kRunUnits, u = idx % kRunUnits;
+      if (rb < nb && u < na * W) {
+        V v = __builtin_nontemporal_load(reinterpret_cast<const V *>(s + (int64_t)rb * d.sb + u));
+        *reinterpret_cast<V *>(&tile[rb * ROW + u]) = v;
+      }
+    }
+    __syncthreads();
+    // store: destination row a holds nb*W contiguous units starting at run b0
+    uint4 *q = dst + dof + b0 * W + a0 * d.da;
+#pragma unroll
+    for (int it = 0; it < kRunTB * kRunUnits / kThreads; ++it) {
+      const int idx = it * kThreads + threadIdx.x;
+      const int ra = idx / (kRunTB * W), m = idx % (kRunTB * W);
+      const int b = m / W, w = m % W;
+      if (ra < na && b < nb) {
+        V v = *reinterpret_cast<const V *>(&tile[b * ROW + ra * W + w]);
+        __builtin_nontemporal_store(v, reinterpret_cast<V *>(q + (int64_t)ra * d.da + m));
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- generic --
 template <int ES>
 __global__ void __launch_bounds__(kThreads)
@@ -186,9 +270,9 @@ bool fill_decomp(Decomp &d, const std::vector<Dim> &outer_to_inner) {
   return true;
 }
 
-int grid_for(uint64_t work_items, uint64_t per_block) {
+int grid_for(uint64_t work_items, uint64_t per_block, uint64_t cap = 256ull * 16) {
   uint64_t g = (work_items + per_block - 1) / per_block;
-  const uint64_t cap = 256ull * 16;  // 256 CUs x 16 resident-ish blocks, then grid-stride
+  // default cap: 256 CUs x 16 resident-ish blocks, then grid-stride
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
@@ -220,13 +304,13 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   const uint64_t vpr = (uint64_t)(row_bytes / VB);
   const uint64_t total = rows * vpr;
   const FastDiv fv = make_fastdiv(vpr);
-  const int grid = grid_for(total, (uint64_t)kThreads * kUnroll);
+  const int grid = grid_for(total, (uint64_t)kRcThreads * kUnroll, BM_RC_GRIDCAP);
   switch (VB) {
-    case 16: k_rowcopy<16><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    case 8: k_rowcopy<8><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    case 4: k_rowcopy<4><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    case 2: k_rowcopy<2><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    default: k_rowcopy<1><<<grid, kThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
   }
   return BM_OK;
 }
@@ -342,6 +426,59 @@ int launch_generic(const char *src, char *dst, const std::vector<Dim> &dims, int
   return BM_OK;
 }
 
+
+// Runs transpose applies when the innermost (both-contiguous) run is W 16-B
+// units with 2 <= W <= 16, dim B (next in destination order) continues the
+// destination run and some other dim A continues the source run.
+int try_transpose_runs(const char *src, char *dst, const std::vector<Dim> &dims, int es,
+                       hipStream_t st) {
+  const int n = (int)dims.size();
+  if (n < 3) return 1;
+  const Dim &in = dims.back();
+  const int64_t rb = in.n * es;
+  if (rb % 16 || rb < 32 || rb > BM_RUNS_MAXB) return 1;
+  if (!aligned(src, 16) || !aligned(dst, 16)) return 1;
+  const int B = n - 2;
+  if (dims[B].ds != in.n) return 1;
+  int A = -1;
+  for (int k = 0; k < n - 1; ++k)
+    if (k != B && dims[k].ss == in.n) A = k;
+  if (A < 0) return 1;
+  for (int k = 0; k < n - 1; ++k)
+    if ((dims[k].ss * es) % 16 || (dims[k].ds * es) % 16) return 1;
+  const int W = (int)(rb / 16);
+  const int64_t u = 16 / es;  // elements per unit
+  RunsDesc d;
+  d.La = dims[A].n;
+  d.Lb = dims[B].n;
+  d.sb = dims[B].ss / u;
+  d.da = dims[A].ds / u;
+  std::vector<Dim> batch;
+  for (int k = 0; k < n - 1; ++k)
+    if (k != A && k != B) batch.push_back({dims[k].n, dims[k].ss / u, dims[k].ds / u});
+  if (!fill_decomp(d.batch, batch)) return 1;
+  const int TA = kRunUnits / W;
+  const uint64_t ntA = (uint64_t)((d.La + TA - 1) / TA);
+  const uint64_t ntB = (uint64_t)((d.Lb + kRunTB - 1) / kRunTB);
+  uint64_t nbatch = 1;
+  for (const Dim &x : batch) nbatch *= (uint64_t)x.n;
+  d.ntB = make_fastdiv(ntB);
+  d.ntAB = make_fastdiv(ntA * ntB);
+  d.ntiles = ntA * ntB * nbatch;
+  uint64_t g = d.ntiles;
+  if (g > 0x7fffffffull) g = 0x7fffffffull;
+  const uint4 *s = (const uint4 *)src;
+  uint4 *t = (uint4 *)dst;
+  switch (W) {
+    case 2: k_transpose_runs<2><<<(int)g, kThreads, 0, st>>>(s, t, d); break;
+    case 4: k_transpose_runs<4><<<(int)g, kThreads, 0, st>>>(s, t, d); break;
+    case 8: k_transpose_runs<8><<<(int)g, kThreads, 0, st>>>(s, t, d); break;
+    case 16: k_transpose_runs<16><<<(int)g, kThreads, 0, st>>>(s, t, d); break;
+    default: return 1;  // other widths: rowcopy
+  }
+  return 0;
+}
+
 // Canonical form: unit dims dropped, dims ordered by destination stride
 // (outermost first), mergeable neighbours fused.
 std::vector<Dim> canonicalize(std::vector<Dim> dims) {
@@ -402,7 +539,8 @@ extern "C" int bm_copy_strided(const void *src_, void *dst_, int ndim, const int
   int rc;
   const Dim &in = c.back();
   if (in.ss == 1 && in.ds == 1) {
-    rc = launch_rowcopy(src, dst, c, es, st);
+    rc = (BM_RUNS_T && try_transpose_runs(src, dst, c, es, st) == 0) ? BM_OK
+                                                                    : launch_rowcopy(src, dst, c, es, st);
   } else {
     int a = -1;
     if (in.ds == 1 && es <= 8)

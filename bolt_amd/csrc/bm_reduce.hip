@@ -31,7 +31,13 @@ constexpr int kThreads = 256;
 #endif
 constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
 
-enum Mode { M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4 };
+enum Mode { M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4, M_MAX = 5, M_MIN = 6 };
+
+// "bit modes" keep a uint64 accumulator: modular integer sum, OR (bool sum),
+// and max / min holding the element's own bits (typed compares below).
+template <int MODE> constexpr bool bit_mode() {
+  return MODE == M_ISUM || MODE == M_OR || MODE == M_MAX || MODE == M_MIN;
+}
 
 template <typename T> __device__ __forceinline__ double to_f64(T x) { return (double)x; }
 template <> __device__ __forceinline__ double to_f64<_Float16>(_Float16 x) { return (double)(float)x; }
@@ -43,6 +49,55 @@ template <> __device__ __forceinline__ uint64_t to_u64<uint64_t>(uint64_t x) { r
 template <> __device__ __forceinline__ uint64_t to_u64<uint8_t>(uint8_t x) { return x; }
 template <> __device__ __forceinline__ uint64_t to_u64<uint16_t>(uint16_t x) { return x; }
 template <> __device__ __forceinline__ uint64_t to_u64<uint32_t>(uint32_t x) { return x; }
+
+template <typename T> __device__ __forceinline__ uint64_t bits_of(T x) {
+  uint64_t u = 0;
+  __builtin_memcpy(&u, &x, sizeof(T));
+  return u;
+}
+template <typename T> __device__ __forceinline__ T from_bits(uint64_t u) {
+  T x;
+  __builtin_memcpy(&x, &u, sizeof(T));
+  return x;
+}
+template <typename T> __device__ __forceinline__ bool is_nan(T x) { return x != x; }
+
+// numpy.maximum / numpy.minimum: a NaN operand wins (NaNs propagate)
+template <typename T, bool MAX> __device__ __forceinline__ T pick(T a, T b) {
+  if (is_nan(a)) return a;
+  if (is_nan(b)) return b;
+  return MAX ? (b > a ? b : a) : (b < a ? b : a);
+}
+
+template <typename T> struct Lim;
+template <> struct Lim<uint8_t> { static __device__ uint8_t lo() { return 0; } static __device__ uint8_t hi() { return 0xff; } };
+template <> struct Lim<int8_t> { static __device__ int8_t lo() { return -128; } static __device__ int8_t hi() { return 127; } };
+template <> struct Lim<uint16_t> { static __device__ uint16_t lo() { return 0; } static __device__ uint16_t hi() { return 0xffff; } };
+template <> struct Lim<int16_t> { static __device__ int16_t lo() { return -32768; } static __device__ int16_t hi() { return 32767; } };
+template <> struct Lim<uint32_t> { static __device__ uint32_t lo() { return 0; } static __device__ uint32_t hi() { return 0xffffffffu; } };
+template <> struct Lim<int32_t> { static __device__ int32_t lo() { return (-2147483647 - 1); } static __device__ int32_t hi() { return 2147483647; } };
+template <> struct Lim<uint64_t> { static __device__ uint64_t lo() { return 0; } static __device__ uint64_t hi() { return ~0ull; } };
+template <> struct Lim<int64_t> { static __device__ int64_t lo() { return (-9223372036854775807ll - 1); } static __device__ int64_t hi() { return 9223372036854775807ll; } };
+template <> struct Lim<_Float16> { static __device__ _Float16 lo() { return -__builtin_inff16(); } static __device__ _Float16 hi() { return __builtin_inff16(); } };
+template <> struct Lim<float> { static __device__ float lo() { return -__builtin_inff(); } static __device__ float hi() { return __builtin_inff(); } };
+template <> struct Lim<double> { static __device__ double lo() { return -__builtin_inf(); } static __device__ double hi() { return __builtin_inf(); } };
+
+// identity, element conversion and combination of the bit modes
+template <typename T, int MODE> __device__ __forceinline__ uint64_t bident() {
+  if (MODE == M_MAX) return bits_of<T>(Lim<T>::lo());
+  if (MODE == M_MIN) return bits_of<T>(Lim<T>::hi());
+  return 0;
+}
+template <typename T, int MODE> __device__ __forceinline__ uint64_t belem(T x) {
+  if (MODE == M_ISUM) return to_u64(x);
+  if (MODE == M_OR) return (uint64_t)(x != 0);
+  return bits_of<T>(x);
+}
+template <typename T, int MODE> __device__ __forceinline__ uint64_t bop(uint64_t a, uint64_t b) {
+  if (MODE == M_ISUM) return a + b;
+  if (MODE == M_OR) return a | b;
+  return bits_of<T>(pick<T, MODE == M_MAX>(from_bits<T>(a), from_bits<T>(b)));
+}
 
 // Per-lane accumulator for one output column.
 template <int MODE> struct Acc;
@@ -101,14 +156,16 @@ __device__ __forceinline__ void store_out(void *out, int64_t idx, double v, int 
 }
 
 __device__ __forceinline__ void store_int(void *out, int64_t idx, uint64_t v, int dt) {
-  switch (dt) {
+  switch (dt) {  // the low bytes of v, by the element width
     case BM_BOOL:
     case BM_U8:
     case BM_I8: ((uint8_t *)out)[idx] = (uint8_t)v; break;
     case BM_U16:
-    case BM_I16: ((uint16_t *)out)[idx] = (uint16_t)v; break;
+    case BM_I16:
+    case BM_F16: ((uint16_t *)out)[idx] = (uint16_t)v; break;
     case BM_U32:
-    case BM_I32: ((uint32_t *)out)[idx] = (uint32_t)v; break;
+    case BM_I32:
+    case BM_F32: ((uint32_t *)out)[idx] = (uint32_t)v; break;
     default: ((uint64_t *)out)[idx] = v; break;
   }
 }
@@ -132,7 +189,7 @@ struct Sink {
 template <int MODE>
 __device__ __forceinline__ void emit(const Sink &sk, int64_t e, double n, double mean, double m2,
                                      uint64_t u) {
-  if (MODE == M_ISUM || MODE == M_OR) {
+  if (bit_mode<MODE>()) {
     if (sk.final_out) store_int(sk.out, e, u, sk.out_dtype);
     else ((uint64_t *)sk.p0)[e] = u;
   } else if (MODE == M_FSUM) {
@@ -178,7 +235,7 @@ __global__ void __launch_bounds__(kThreads)
   double fs[VEC];
   uint64_t us[VEC];
 #pragma unroll
-  for (int k = 0; k < VEC; ++k) { acc[k].init(); fs[k] = 0.0; us[k] = 0; }
+  for (int k = 0; k < VEC; ++k) { acc[k].init(); fs[k] = 0.0; us[k] = bident<T, MODE>(); }
 
   if (active) {
     const T *base = src + ((int64_t)o * d.R) * d.I + col0;
@@ -206,10 +263,9 @@ __global__ void __launch_bounds__(kThreads)
         } else if (MODE == M_FSUM) {
           fs[k] += to_f64(v0[k]); fs[k] += to_f64(v1[k]);
           fs[k] += to_f64(v2[k]); fs[k] += to_f64(v3[k]);
-        } else if (MODE == M_ISUM) {
-          us[k] += to_u64(v0[k]) + to_u64(v1[k]) + to_u64(v2[k]) + to_u64(v3[k]);
         } else {
-          us[k] |= (uint64_t)((v0[k] != 0) | (v1[k] != 0) | (v2[k] != 0) | (v3[k] != 0));
+          us[k] = bop<T, MODE>(us[k], bop<T, MODE>(bop<T, MODE>(belem<T, MODE>(v0[k]), belem<T, MODE>(v1[k])),
+                                                   bop<T, MODE>(belem<T, MODE>(v2[k]), belem<T, MODE>(v3[k]))));
         }
       }
     }
@@ -220,8 +276,7 @@ __global__ void __launch_bounds__(kThreads)
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc[k].add(to_f64(v[k]));
         else if (MODE == M_FSUM) fs[k] += to_f64(v[k]);
-        else if (MODE == M_ISUM) us[k] += to_u64(v[k]);
-        else us[k] |= (uint64_t)(v[k] != 0);
+        else us[k] = bop<T, MODE>(us[k], belem<T, MODE>(v[k]));
       }
     }
   }
@@ -261,12 +316,9 @@ __global__ void __launch_bounds__(kThreads)
             m_[k] = ma; q_[k] = qa;
           } else if (MODE == M_FSUM) {
             m_[k] += mb;
-          } else if (MODE == M_ISUM) {
-            m_[k] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m_[k]) +
-                                                   __builtin_bit_cast(uint64_t, mb));
           } else {
-            m_[k] = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m_[k]) |
-                                                   __builtin_bit_cast(uint64_t, mb));
+            m_[k] = __builtin_bit_cast(double, bop<T, MODE>(__builtin_bit_cast(uint64_t, m_[k]),
+                                                            __builtin_bit_cast(uint64_t, mb)));
           }
         }
         n0 += nb;
@@ -308,7 +360,7 @@ __global__ void __launch_bounds__(kThreads)
   Acc<(MODE == M_MOM) ? M_MOM : M_MEAN> acc;
   acc.init();
   double fs = 0.0;
-  uint64_t us = 0;
+  uint64_t us = bident<T, MODE>();
   int64_t j = r_lo + (int64_t)lane * VEC;
   const int64_t stride = 64 * VEC;
   if ((MODE == M_MEAN || MODE == M_MOM) && j < r_hi) {
@@ -335,8 +387,7 @@ __global__ void __launch_bounds__(kThreads)
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[u][k]));
         else if (MODE == M_FSUM) fs += to_f64(v[u][k]);
-        else if (MODE == M_ISUM) us += to_u64(v[u][k]);
-        else us |= (uint64_t)(v[u][k] != 0);
+        else us = bop<T, MODE>(us, belem<T, MODE>(v[u][k]));
       }
     }
   }
@@ -348,15 +399,13 @@ __global__ void __launch_bounds__(kThreads)
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[k]));
         else if (MODE == M_FSUM) fs += to_f64(v[k]);
-        else if (MODE == M_ISUM) us += to_u64(v[k]);
-        else us |= (uint64_t)(v[k] != 0);
+        else us = bop<T, MODE>(us, belem<T, MODE>(v[k]));
       }
     } else {
       for (int64_t k = j; k < r_hi; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(row[k]));
         else if (MODE == M_FSUM) fs += to_f64(row[k]);
-        else if (MODE == M_ISUM) us += to_u64(row[k]);
-        else us |= (uint64_t)(row[k] != 0);
+        else us = bop<T, MODE>(us, belem<T, MODE>(row[k]));
       }
     }
   }
@@ -382,10 +431,9 @@ __global__ void __launch_bounds__(kThreads)
     } else if (MODE == M_FSUM) {
       const double mb = __shfl_xor(m, off);
       m = (lane & off) ? (mb + m) : (m + mb);
-    } else if (MODE == M_ISUM) {
-      us += (uint64_t)__shfl_xor((long long)us, off);
     } else {
-      us |= (uint64_t)__shfl_xor((long long)us, off);
+      const uint64_t ub = (uint64_t)__shfl_xor((long long)us, off);
+      us = (lane & off) ? bop<T, MODE>(ub, us) : bop<T, MODE>(us, ub);
     }
   }
   if (lane != 0) return;
@@ -406,13 +454,14 @@ struct CombDesc {
   int64_t counts[64];
 };
 
-template <int MODE>
+template <int MODE, typename T>
 __global__ void __launch_bounds__(kThreads)
     k_red_combine(const double *__restrict__ p0, const double *__restrict__ p1, CombDesc d, Sink sk) {
   const int64_t step = (int64_t)gridDim.x * kThreads;
   for (int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x; e < d.nout; e += step) {
     double n = 0.0, m = 0.0, q = 0.0;
     uint64_t u = 0;
+    bool first = true;
     for (int64_t p = 0; p < d.nparts; ++p) {
       const double nb = d.explicit_counts
                             ? (double)d.counts[p]
@@ -424,11 +473,11 @@ __global__ void __launch_bounds__(kThreads)
       } else if (MODE == M_FSUM) {
         m += p0[at];
         n += nb;
-      } else if (MODE == M_ISUM) {
-        u += ((const uint64_t *)p0)[at];
       } else {
-        u |= ((const uint64_t *)p0)[at];
+        const uint64_t b = ((const uint64_t *)p0)[at];
+        u = first ? b : bop<T, MODE>(u, b);
       }
+      first = false;
     }
     emit<MODE>(sk, e, n, m, q, u);
   }
@@ -449,11 +498,14 @@ bool is_float(int dt) { return dt == BM_F16 || dt == BM_F32 || dt == BM_F64; }
 int mode_of(int stat, int dt) {
   if (stat == BM_STAT_MEAN) return M_MEAN;
   if (stat == BM_STAT_VAR || stat == BM_STAT_STD) return M_MOM;
+  if (stat == BM_STAT_MAX) return M_MAX;
+  if (stat == BM_STAT_MIN) return M_MIN;
   if (is_float(dt)) return M_FSUM;
   if (dt == BM_BOOL) return M_OR;
   return M_ISUM;
 }
 int planes_of(int mode) { return mode == M_MOM ? 2 : 1; }
+bool bit_mode_host(int mode) { return mode == M_ISUM || mode == M_OR || mode == M_MAX || mode == M_MIN; }
 
 struct RedPlan {
   bool rows;
@@ -585,27 +637,49 @@ int launch_main(int mode, int dt, const RedPlan &p, const void *src, int64_t O, 
     case M_MOM: return launch_main_m<M_MOM>(dt, p, src, O, R, I, sk, st);
     case M_FSUM: return launch_main_m<M_FSUM>(dt, p, src, O, R, I, sk, st);
     case M_ISUM: return launch_main_m<M_ISUM>(dt, p, src, O, R, I, sk, st);
+    case M_MAX: return launch_main_m<M_MAX>(dt, p, src, O, R, I, sk, st);
+    case M_MIN: return launch_main_m<M_MIN>(dt, p, src, O, R, I, sk, st);
     default: return launch_main_m<M_OR>(dt, p, src, O, R, I, sk, st);
   }
 }
 
-int launch_combine(int mode, const double *p0, const double *p1, const CombDesc &cd, Sink sk,
+template <int MODE>
+void launch_combine_m(int dt, int g, const double *p0, const double *p1, const CombDesc &cd, Sink sk,
+                      hipStream_t st) {
+  switch (dt) {  // only max/min look at the element type
+    case BM_BOOL: case BM_U8: k_red_combine<MODE, uint8_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_I8: k_red_combine<MODE, int8_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_U16: k_red_combine<MODE, uint16_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_I16: k_red_combine<MODE, int16_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_U32: k_red_combine<MODE, uint32_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_I32: k_red_combine<MODE, int32_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_U64: k_red_combine<MODE, uint64_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_I64: k_red_combine<MODE, int64_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_F16: k_red_combine<MODE, _Float16><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_F32: k_red_combine<MODE, float><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    default: k_red_combine<MODE, double><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+  }
+}
+
+int launch_combine(int mode, int dt, const double *p0, const double *p1, const CombDesc &cd, Sink sk,
                    hipStream_t st) {
   int64_t g = cdiv(cd.nout, kThreads);
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   switch (mode) {
-    case M_MEAN: k_red_combine<M_MEAN><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_MOM: k_red_combine<M_MOM><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_FSUM: k_red_combine<M_FSUM><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_ISUM: k_red_combine<M_ISUM><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    default: k_red_combine<M_OR><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_MEAN: k_red_combine<M_MEAN, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_MOM: k_red_combine<M_MOM, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_FSUM: k_red_combine<M_FSUM, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_ISUM: k_red_combine<M_ISUM, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_OR: k_red_combine<M_OR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_MAX: launch_combine_m<M_MAX>(dt, (int)g, p0, p1, cd, sk, st); break;
+    default: launch_combine_m<M_MIN>(dt, (int)g, p0, p1, cd, sk, st); break;
   }
   return BM_OK;
 }
 
 int check_args(int stat, int dt, int64_t O, int64_t R, int64_t I, const char *who) {
-  if (stat < BM_STAT_MEAN || stat > BM_STAT_SUM || dtype_size(dt) == 0) {
+  if (stat < BM_STAT_MEAN || stat > BM_STAT_MIN || dtype_size(dt) == 0) {
     bm_set_error("%s: bad stat %d / dtype %d", who, stat, dt);
     return BM_E_ARG;
   }
@@ -662,7 +736,7 @@ int run_reduce(int stat, const void *src, int dt, int64_t O, int64_t R, int64_t 
   cd.R = R;
   cd.rchunk = p.rchunk;
   cd.explicit_counts = 0;
-  rc = launch_combine(mode, w0, w1, cd, sk, st);
+  rc = launch_combine(mode, dt, w0, w1, cd, sk, st);
   if (rc) return rc;
   return check_launch(who);
 }
@@ -690,8 +764,8 @@ extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int
   if (rc) return rc;
   if (!src || !out) { bm_set_error("bm_reduce: null pointer"); return BM_E_ARG; }
   const int mode = mode_of(stat, in_dtype);
-  if (mode == M_ISUM || mode == M_OR) {
-    if (out_dtype != in_dtype) { bm_set_error("bm_reduce: integer sum keeps the input dtype"); return BM_E_ARG; }
+  if (bit_mode_host(mode)) {
+    if (out_dtype != in_dtype) { bm_set_error("bm_reduce: integer sum / max / min keep the input dtype"); return BM_E_ARG; }
   } else if (!is_float(out_dtype)) {
     bm_set_error("bm_reduce: out_dtype must be a float dtype");
     return BM_E_ARG;
@@ -706,7 +780,7 @@ extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int
 }
 
 extern "C" int bm_reduce_state_bytes(int stat, int in_dtype, int64_t nout, size_t *bytes) {
-  if (!bytes || nout < 0 || stat < BM_STAT_MEAN || stat > BM_STAT_SUM || dtype_size(in_dtype) == 0) {
+  if (!bytes || nout < 0 || stat < BM_STAT_MEAN || stat > BM_STAT_MIN || dtype_size(in_dtype) == 0) {
     bm_set_error("bm_reduce_state_bytes: bad arguments");
     return BM_E_ARG;
   }
@@ -734,14 +808,14 @@ extern "C" int bm_reduce_state(int stat, const void *src, int in_dtype, int64_t 
 
 extern "C" int bm_reduce_combine(int stat, int in_dtype, const void *states, const int64_t *counts,
                                  int nparts, int64_t nout, void *out, int out_dtype, void *stream) {
-  if (stat < BM_STAT_MEAN || stat > BM_STAT_SUM || dtype_size(in_dtype) == 0 || nparts < 1 ||
+  if (stat < BM_STAT_MEAN || stat > BM_STAT_MIN || dtype_size(in_dtype) == 0 || nparts < 1 ||
       nparts > 64 || nout < 1 || !states || !counts || !out) {
     bm_set_error("bm_reduce_combine: bad arguments");
     return BM_E_ARG;
   }
   const int mode = mode_of(stat, in_dtype);
-  if (mode == M_ISUM || mode == M_OR) {
-    if (out_dtype != in_dtype) { bm_set_error("bm_reduce_combine: integer sum keeps the input dtype"); return BM_E_ARG; }
+  if (bit_mode_host(mode)) {
+    if (out_dtype != in_dtype) { bm_set_error("bm_reduce_combine: integer sum / max / min keep the input dtype"); return BM_E_ARG; }
   } else if (!is_float(out_dtype)) {
     bm_set_error("bm_reduce_combine: out_dtype must be a float dtype");
     return BM_E_ARG;
@@ -758,7 +832,7 @@ extern "C" int bm_reduce_combine(int stat, int in_dtype, const void *states, con
   sk.stat = stat;
   sk.final_out = 1;
   const double *p0 = (const double *)states;
-  int rc = launch_combine(mode, p0, p0 + nout, cd, sk, (hipStream_t)stream);
+  int rc = launch_combine(mode, in_dtype, p0, p0 + nout, cd, sk, (hipStream_t)stream);
   if (rc) return rc;
   return check_launch("bm_reduce_combine");
 }

@@ -290,11 +290,10 @@ class BoltArrayMI355X(BoltArray):
         if the reduced axes are not one block they are first permuted to the
         front (what _align's swap does physically, array.py:85-115).
         """
-        import torch
         axset = sorted(set(int(a) for a in axis))
         kept = [i for i in range(self.ndim) if i not in axset]
         out_shape = tuple(self._shape[i] for i in kept)
-        if stat == _lib.STAT_SUM:
+        if stat in (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN):
             out_dtype = self._dtype
         else:
             out_dtype = stat_dtype(self._dtype, out_shape)
@@ -372,15 +371,18 @@ class BoltArrayMI355X(BoltArray):
     def reduce(self, func, axis=(0,), keepdims=False):
         """Reduce with ``func`` over ``axis`` (array.py:243-282).
 
-        Only elementwise addition (operator.add / numpy.add: the path sum()
-        takes) runs on the GPU; other functions are outside this backend.
+        The reductions sum/max/min take -- operator.add / numpy.add,
+        numpy.maximum, numpy.minimum -- run on the GPU in the input dtype;
+        arbitrary Python functions are outside this backend.
         """
         import operator
-        if func not in (operator.add, np.add):
-            raise NotImplementedError("the mi355x mode reduces with addition only (sum); got %r" % (func,))
+        stat = {operator.add: _lib.STAT_SUM, np.add: _lib.STAT_SUM,
+                np.maximum: _lib.STAT_MAX, np.minimum: _lib.STAT_MIN}.get(func)
+        if stat is None:
+            raise NotImplementedError("the mi355x mode reduces with add / maximum / minimum; got %r" % (func,))
         axis = tupleize(axis)
         inshape(self.shape, axis)
-        arr, _ = self._reduced(axis, _lib.STAT_SUM)
+        arr, _ = self._reduced(axis, stat)
         if arr.ndim == 0:
             arr = arr[()]
         if keepdims:
@@ -408,6 +410,14 @@ class BoltArrayMI355X(BoltArray):
         """Sum over ``axis`` in the input dtype (array.py:381-395; integer sums wrap)."""
         import operator
         return self._stat(axis, func=operator.add, keepdims=keepdims)
+
+    def max(self, axis=None, keepdims=False):
+        """Maximum over ``axis`` (array.py:397-411): numpy.maximum, NaNs propagate."""
+        return self._stat(axis, func=np.maximum, keepdims=keepdims)
+
+    def min(self, axis=None, keepdims=False):
+        """Minimum over ``axis`` (array.py:413-427): numpy.minimum, NaNs propagate."""
+        return self._stat(axis, func=np.minimum, keepdims=keepdims)
 
     # -------------------------------------------------------------- egress
     def _gathered_bytes(self):

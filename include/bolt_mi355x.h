@@ -57,6 +57,8 @@ extern "C" {
 #define BM_STAT_VAR 1    /* StatCounter.variance  statcounter.py:119-125 */
 #define BM_STAT_STD 2    /* StatCounter.stdev     statcounter.py:127-130 */
 #define BM_STAT_SUM 3    /* reduce(operator.add)  array.py:243-282, :381-395 */
+#define BM_STAT_MAX 4    /* reduce(numpy.maximum) array.py:397-411 (NaN propagates) */
+#define BM_STAT_MIN 5    /* reduce(numpy.minimum) array.py:413-427 (NaN propagates) */
 
 /* Version of this ABI (BM_ABI_VERSION).  Host code refuses a mismatch. */
 int bm_abi_version(void);
@@ -110,8 +112,9 @@ int bm_permute(const void *src, void *dst, int ndim, const int64_t *shape,
  * blocks and chunks in a fixed order: deterministic) and round once to
  * out_dtype.  SUM over integer dtypes is modular in the input width
  * (numpy add of same-dtype arrays wraps: the reference's treeReduce(add));
- * SUM over BM_BOOL is logical OR (numpy bool add).
- * out_dtype: BM_F16/BM_F32/BM_F64 for MEAN/VAR/STD; in_dtype for SUM.
+ * SUM over BM_BOOL is logical OR (numpy bool add).  MAX / MIN compare in the
+ * input dtype with numpy.maximum / numpy.minimum semantics (a NaN wins).
+ * out_dtype: BM_F16/BM_F32/BM_F64 for MEAN/VAR/STD; in_dtype for SUM/MAX/MIN.
  * Population variance (M2/n), std = sqrt(var), as statcounter.py:119-130.
  */
 int bm_reduce_workspace_bytes(int stat, int in_dtype, int64_t O, int64_t R,
@@ -126,7 +129,8 @@ int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
  * StatCounter of array.py:321-322).  `state` receives, for O*I outputs:
  *   MEAN/VAR/STD: two float64 planes, mean[O*I] then M2[O*I] (count = R);
  *   SUM float:    one float64 plane (the sum);
- *   SUM int/bool: one uint64 plane (modular sum / OR).
+ *   SUM int/bool: one uint64 plane (modular sum / OR);
+ *   MAX / MIN:    one uint64 plane holding the element's bits.
  * bm_reduce_state_bytes gives the state size in bytes.
  */
 int bm_reduce_state_bytes(int stat, int in_dtype, int64_t nout, size_t *bytes);

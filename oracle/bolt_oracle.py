@@ -419,12 +419,13 @@ def stat(rs, name, axis=None, keepdims=False):
     return arr
 
 
-def sum_(rs, axis=None, keepdims=False):
-    """BoltArraySpark.reduce(add) (array.py:243-282): treeReduce of `+` in the input dtype."""
+def reduce_(rs, func, axis=None, keepdims=False):
+    """BoltArraySpark.reduce (array.py:243-282): treeReduce of ``func`` over the
+    aligned records (per partition, then across partitions), input dtype."""
     axis = _normalise_axis(rs, axis)
     sw = align(rs, axis)
-    partials = [_reduce(lambda a, b: a + b, [v for _, v in p]) for p in sw.parts if p]
-    arr = _reduce(lambda a, b: a + b, partials)
+    partials = [_reduce(func, [v for _, v in p]) for p in sw.parts if p]
+    arr = _reduce(func, partials)
     if keepdims:
         for i in axis:
             arr = np.expand_dims(arr, axis=i)
@@ -433,6 +434,21 @@ def sum_(rs, axis=None, keepdims=False):
     if arr.shape == (1,):
         return arr[0]
     return arr
+
+
+def sum_(rs, axis=None, keepdims=False):
+    """sum = reduce(operator.add) (array.py:381-395)."""
+    return reduce_(rs, lambda a, b: a + b, axis, keepdims)
+
+
+def max_(rs, axis=None, keepdims=False):
+    """max = reduce(numpy.maximum) (array.py:397-411)."""
+    return reduce_(rs, np.maximum, axis, keepdims)
+
+
+def min_(rs, axis=None, keepdims=False):
+    """min = reduce(numpy.minimum) (array.py:413-427)."""
+    return reduce_(rs, np.minimum, axis, keepdims)
 
 
 def repartition(rs, n):

@@ -11,7 +11,7 @@ with the same output-dtype and modular-integer rules as the kernels.
 """
 import numpy as np
 
-STAT_MEAN, STAT_VAR, STAT_STD, STAT_SUM = range(4)
+STAT_MEAN, STAT_VAR, STAT_STD, STAT_SUM, STAT_MAX, STAT_MIN = range(6)
 _CODES = [np.bool_, np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64,
           np.int64, np.float16, np.float32, np.float64]
 
@@ -23,6 +23,19 @@ def _np(t):
 def _view(buf, off, shape, strides, es):
     return np.ndarray(tuple(int(s) for s in shape), dtype=np.dtype((np.void, es)), buffer=buf,
                       offset=int(off), strides=tuple(int(s) * es for s in strides))
+
+
+def _bits64(a):
+    """Elements' bits in the low bytes of uint64 slots (the max/min state layout)."""
+    a = np.ascontiguousarray(a)
+    out = np.zeros(a.size, dtype=np.uint64)
+    out.view(np.uint8).reshape(a.size, 8)[:, :a.itemsize] = a.view(np.uint8).reshape(a.size, a.itemsize)
+    return out
+
+
+def _unbits64(u, dt):
+    u = np.ascontiguousarray(u, dtype=np.uint64)
+    return u.view(np.uint8).reshape(u.size, 8)[:, :dt.itemsize].copy().view(dt).reshape(-1)
 
 
 class CpuBackend(object):
@@ -45,6 +58,10 @@ class CpuBackend(object):
     def _planes(self, stat, code, x):
         """x: (O, R, I) in the input dtype -> state planes (list of arrays (O*I,))."""
         dt = np.dtype(_CODES[code])
+        if stat in (STAT_MAX, STAT_MIN):
+            f = np.maximum if stat == STAT_MAX else np.minimum
+            r = f.reduce(x, axis=1).reshape(-1)
+            return [_bits64(r)]
         if stat == STAT_SUM:
             if dt == np.bool_:
                 return [x.any(axis=1).reshape(-1).astype(np.uint64)]
@@ -60,6 +77,9 @@ class CpuBackend(object):
         dt = np.dtype(_CODES[code])
         odt = np.dtype(_CODES[out_code])
         o = _np(out).view(odt)
+        if stat in (STAT_MAX, STAT_MIN):
+            o[...] = _unbits64(planes[0], dt)
+            return
         if stat == STAT_SUM:
             if dt.kind in 'iub':
                 o[...] = planes[0].astype(dt) if dt != np.bool_ else planes[0] != 0
@@ -77,7 +97,7 @@ class CpuBackend(object):
         self._finish(stat, code, self._planes(stat, code, x), float(R), out, out_code)
 
     def state_bytes(self, stat, code, nout):
-        mom = stat in (STAT_VAR, STAT_STD)
+        mom = stat in (STAT_VAR, STAT_STD)  # max / min / sum / mean: one 8-byte plane
         return (2 if mom else 1) * nout * 8
 
     def reduce_state(self, stat, src, code, O, R, I, state):
@@ -98,10 +118,16 @@ class CpuBackend(object):
         n, m, q = 0.0, np.zeros(nout), np.zeros(nout)
         acc_u = np.zeros(nout, dtype=np.uint64)
         acc_f = np.zeros(nout)
+        acc_m = None
         for p, c in enumerate(counts):
             if c <= 0:
                 continue
             part = buf[p * per:(p + 1) * per]
+            if stat in (STAT_MAX, STAT_MIN):
+                f = np.maximum if stat == STAT_MAX else np.minimum
+                v = _unbits64(part[:nout * 8].view(np.uint64), dt)
+                acc_m = v.copy() if acc_m is None else f(acc_m, v)
+                continue
             if stat == STAT_SUM:
                 if dt.kind in 'iub':
                     u = part[:nout * 8].view(np.uint64)
@@ -119,7 +145,9 @@ class CpuBackend(object):
                 m = m + d * (c / tot)
                 q = q + qb + d * d * (n * c / tot)
                 n = tot
-        if stat == STAT_SUM:
+        if stat in (STAT_MAX, STAT_MIN):
+            planes = [_bits64(acc_m)]
+        elif stat == STAT_SUM:
             planes = [acc_u] if dt.kind in 'iub' else [acc_f]
         else:
             planes = [m, q]

@@ -336,7 +336,7 @@ def gen_stats():
         x = make_input(s)
         for npart in ((8,) if s["shape"] == [100, 64, 64] else (1, 2, 8)):
             b = bolt.array(x, sc, axis=kaxis, npartitions=npart)
-            for name in ("mean", "var", "std", "sum"):
+            for name in ("mean", "var", "std", "sum", "min", "max"):
                 for ax in axes_list:
                     if ax is not None and max(np.atleast_1d(ax)) >= x.ndim:
                         continue

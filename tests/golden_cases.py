@@ -63,6 +63,8 @@ def truth_stat(x, name, axis):
         return v.mean(axis=ax)
     if name == "sum":
         return v.sum(axis=ax)
+    if name in ("min", "max"):
+        return getattr(v, name)(axis=ax)
     var = v.var(axis=ax)
     return var if name == "var" else np.sqrt(var)
 

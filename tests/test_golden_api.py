@@ -148,7 +148,7 @@ def test_stat(case, bctx):
     assert type(got).__name__ == case["result_type"]
     assert str(np.asarray(got).dtype) == case["result_dtype"]
     assert np.asarray(got).shape == want.shape
-    if want.dtype.kind in 'iub':
+    if want.dtype.kind in 'iub' or case["name"] in ("min", "max"):
         assert np.asarray(got).tobytes() == want.tobytes()
     else:
         truth = G.truth_stat(x, case["name"], ax)

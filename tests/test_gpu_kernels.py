@@ -67,8 +67,16 @@ def test_permute_all_perms_4d(dtype):
     ((40, 300, 32), (2, 1, 0)),  # C3 .T shape family
     ((33, 130, 9), (2, 1, 0)),
     ((2, 8, 300), (2, 0, 1)),
+    # kept innermost run of 32-256 B with the two axes around it swapped (runs transpose)
+    ((300, 70, 32), (1, 0, 2)),
+    ((50, 33, 8), (1, 0, 2)),
+    ((17, 40, 4), (1, 0, 2)),
+    ((9, 70, 64), (1, 0, 2)),
+    ((6, 40, 30, 16), (0, 2, 1, 3)),
+    ((40, 7, 30, 16), (2, 1, 0, 3)),
+    ((130, 3, 129, 32), (2, 1, 0, 3)),
 ])
-@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64])
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64, np.complex128])
 def test_permute_shapes(shape, perm, dtype):
     import torch
     be = _be()

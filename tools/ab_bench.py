@@ -79,7 +79,21 @@ class Reduce(object):
         assert rc == 0, lib.bm_last_error()
 
 
+class Copy(object):
+    def __init__(self, nbytes):
+        self.n = nbytes
+        self.src = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty_like(self.src)
+        self.bytes = 2 * nbytes
+
+    def __call__(self, lib):
+        rc = lib.bm_copy_strided(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()), 1,
+                                 i64([self.n // 4]), i64([1]), i64([1]), 4, stream())
+        assert rc == 0, lib.bm_last_error()
+
+
 OPS = {
+    "c2_copy": lambda: Copy(2097152000),
     "c2_swap": lambda: Permute((2000, 512 * 512), (1, 0), np.float32),
     "c2_mean_rows": lambda: Reduce(0, 512 * 512, 2000, 1, np.float32, np.float32),
     "c2_std_rows": lambda: Reduce(2, 512 * 512, 2000, 1, np.float32, np.float32),
@@ -87,6 +101,9 @@ OPS = {
     "c2_std_cols": lambda: Reduce(2, 1, 2000, 512 * 512, np.float32, np.float32),
     "c3_swap": lambda: Permute((1024, 256, 256, 32), (1, 2, 0, 3), np.float32),
     "c3_T": lambda: Permute((1024, 256, 256, 32), (3, 2, 1, 0), np.float32),
+    "runs32": lambda: Permute((4096, 4096, 8), (1, 0, 2), np.float32),
+    "runs64": lambda: Permute((4096, 2048, 16), (1, 0, 2), np.float32),
+    "runs128": lambda: Permute((2048, 2048, 32), (1, 0, 2), np.float32),
     "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
     "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
     "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),
