@@ -103,30 +103,41 @@ template <typename T, int MODE> __device__ __forceinline__ uint64_t bop(uint64_t
 template <int MODE> struct Acc;
 
 template <> struct Acc<M_MEAN> {
-  double K, S1;
+  // two interleaved partial sums share the pivot: halves the add chain
+  double K, S1, S1b;
   int64_t n;
-  __device__ void init() { K = 0; S1 = 0; n = 0; }
-  __device__ void first(double x) { K = x; S1 = 0; n = 1; }
+  __device__ void init() { K = 0; S1 = 0; S1b = 0; n = 0; }
+  __device__ void first(double x) { K = x; S1 = 0; S1b = 0; n = 1; }
   __device__ void add(double x) { S1 += x - K; ++n; }
-  __device__ double mean() const { return n ? K + S1 / (double)n : 0.0; }
+  __device__ void add2(double x, double y) { S1 += x - K; S1b += y - K; n += 2; }
+  __device__ double mean() const { return n ? K + (S1 + S1b) / (double)n : 0.0; }
   __device__ double m2() const { return 0.0; }
 };
 
 template <> struct Acc<M_MOM> {
-  double K, S1, S2;
+  double K, S1, S2, S1b, S2b;
   int64_t n;
-  __device__ void init() { K = 0; S1 = 0; S2 = 0; n = 0; }
-  __device__ void first(double x) { K = x; S1 = 0; S2 = 0; n = 1; }
+  __device__ void init() { K = 0; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 0; }
+  __device__ void first(double x) { K = x; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 1; }
   __device__ void add(double x) {
     const double dx = x - K;
     S1 += dx;
     S2 = fma(dx, dx, S2);
     ++n;
   }
-  __device__ double mean() const { return n ? K + S1 / (double)n : 0.0; }
+  __device__ void add2(double x, double y) {
+    const double dx = x - K, dy = y - K;
+    S1 += dx;
+    S2 = fma(dx, dx, S2);
+    S1b += dy;
+    S2b = fma(dy, dy, S2b);
+    n += 2;
+  }
+  __device__ double mean() const { return n ? K + (S1 + S1b) / (double)n : 0.0; }
   __device__ double m2() const {
     if (!n) return 0.0;
-    const double v = S2 - S1 * (S1 / (double)n);
+    const double s1 = S1 + S1b;
+    const double v = (S2 + S2b) - s1 * (s1 / (double)n);
     return v > 0.0 ? v : 0.0;
   }
 };
@@ -383,6 +394,11 @@ __global__ void __launch_bounds__(kThreads)
     for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
 #pragma unroll
     for (int u = 0; u < kRowsUnroll; ++u) {
+      if constexpr ((MODE == M_MEAN || MODE == M_MOM) && VEC % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < VEC; k += 2) acc.add2(to_f64(v[u][k]), to_f64(v[u][k + 1]));
+        continue;
+      }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[u][k]));

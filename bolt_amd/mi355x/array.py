@@ -24,7 +24,8 @@ from bolt_amd.mi355x import _lib
 from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
 from bolt_amd.mi355x.context import contiguous_strides, local_shape
-from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, _empty, to_host
+from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, _empty
+from bolt_amd.mi355x.transfer import to_device, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
 from bolt_amd.utils import tupleize, argpack, inshape, istransposeable
@@ -96,12 +97,11 @@ class BoltArrayMI355X(BoltArray):
         lo, hi = ctx.local_bounds(shape[0])
         rowbytes = int(np.prod(shape[1:], dtype=np.int64)) * es
         if identity:
-            host = arry[lo:hi].reshape(-1).view(np.uint8)
-            data = torch.from_numpy(host).to(dev)
+            data = to_device(arry[lo:hi].reshape(-1).view(np.uint8), dev)
         else:
             # full array to HBM, permuted on the GPU, then this rank's slab of
             # the permuted bytes (the reference's reshape to the old shape).
-            full = torch.from_numpy(arry.reshape(-1).view(np.uint8)).to(dev)
+            full = to_device(arry.reshape(-1).view(np.uint8), dev)
             perm_bytes = _empty(full.numel(), dev)
             if full.numel():
                 backend_for(dev).permute(full, arry.shape, permutation, es, perm_bytes)
@@ -118,7 +118,7 @@ class BoltArrayMI355X(BoltArray):
         n = int(np.prod(lshape, dtype=np.int64))
         data = _empty(n * es, dev)
         if n:
-            unit = torch.from_numpy(np.full(1, value, dtype=dtype).view(np.uint8).copy()).to(dev)
+            unit = to_device(np.full(1, value, dtype=dtype).view(np.uint8), dev)
             backend_for(dev).copy_strided(unit, 0, data, 0, [n], [0], [1], es)
         return cls(data, shape=shape, split=split, dtype=dtype, context=ctx, npartitions=npartitions)
 
@@ -128,7 +128,7 @@ class BoltArrayMI355X(BoltArray):
         dev = ctx.device
         if isinstance(shard, np.ndarray):
             dtype = np.dtype(dtype or shard.dtype)
-            data = torch.from_numpy(np.ascontiguousarray(shard, dtype=dtype).reshape(-1).view(np.uint8)).to(dev)
+            data = to_device(np.ascontiguousarray(shard, dtype=dtype).reshape(-1).view(np.uint8), dev)
         else:
             if dtype is None:
                 raise ValueError("dtype is required for a device shard")

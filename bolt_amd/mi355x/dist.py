@@ -24,22 +24,7 @@ def _empty(nbytes, device):
     return torch.empty(max(0, int(nbytes)), dtype=torch.uint8, device=device)
 
 
-def to_host(t, dtype, shape):
-    """Device bytes -> host ndarray of ``dtype``/``shape`` (the only D2H of the mode).
-
-    GPU tensors go through a page-locked staging buffer from torch's caching
-    host allocator (a DMA, no pageable bounce) on the current stream; the
-    returned array owns that buffer.
-    """
-    import torch
-    dtype = np.dtype(dtype)
-    if t.device.type != "cuda":
-        return t.numpy().view(dtype).reshape(shape)
-    host = torch.empty(t.numel(), dtype=torch.uint8, pin_memory=True)
-    if t.numel():
-        host.copy_(t, non_blocking=True)
-        torch.cuda.current_stream(t.device).synchronize()
-    return host.numpy().view(dtype).reshape(shape)
+from bolt_amd.mi355x.transfer import to_host  # noqa: E402,F401  (re-exported)
 
 
 # Pipeline depth of the swap exchange (None: from the message size, >= 32 MiB

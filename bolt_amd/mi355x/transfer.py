@@ -1,0 +1,105 @@
+"""Host <-> HBM transfers of the mi355x mode (ingest and egress).
+
+The reference moves records driver -> executors with parallelize
+(spark/construct.py:69) and back with collect (array.py:1012-1014).  Here the
+path is PCIe (63 GB/s spec, MI355X_MICROARCH.md): a pageable copy bounces
+through the driver's own staging buffers, so large arrays are staged through
+two page-locked chunks from torch's caching host allocator -- the host memcpy
+of chunk i+1 (split over a few threads; numpy releases the GIL) overlaps the
+DMA of chunk i on the current stream.  Small transfers take one pinned buffer.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+CHUNK = 64 << 20          # bytes per staging chunk
+SMALL = 8 << 20           # below this: one pinned buffer, no pipeline
+THREADS = 4               # host memcpy threads per chunk
+
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        _POOL = ThreadPoolExecutor(max_workers=THREADS, thread_name_prefix="bolt-amd-copy")
+    return _POOL
+
+
+def _par_copy(dst, src):
+    """dst[:] = src for 1-D uint8 arrays, split over the copy threads."""
+    n = src.size
+    if n < (4 << 20):
+        dst[:] = src
+        return
+    step = (n + THREADS - 1) // THREADS
+    futs = [_pool().submit(np.copyto, dst[i:i + step], src[i:i + step]) for i in range(0, n, step)]
+    for f in futs:
+        f.result()
+
+
+def to_device(host, device):
+    """Contiguous host bytes (1-D uint8 ndarray) -> uint8 tensor on ``device``."""
+    import torch
+    host = np.ascontiguousarray(host).reshape(-1).view(np.uint8)
+    if device.type != "cuda":
+        return torch.from_numpy(host.copy())
+    n = host.size
+    out = torch.empty(n, dtype=torch.uint8, device=device)
+    if n == 0:
+        return out
+    stream = torch.cuda.current_stream(device)
+    if n <= SMALL:
+        pin = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        _par_copy(pin.numpy(), host)
+        out.copy_(pin, non_blocking=True)
+        stream.synchronize()
+        return out
+    bufs = [torch.empty(CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    evs = [None, None]
+    for i, lo in enumerate(range(0, n, CHUNK)):
+        hi = min(n, lo + CHUNK)
+        k = i % 2
+        if evs[k] is not None:
+            evs[k].synchronize()  # the DMA that last read this buffer is done
+        _par_copy(bufs[k].numpy()[:hi - lo], host[lo:hi])
+        out[lo:hi].copy_(bufs[k][:hi - lo], non_blocking=True)
+        evs[k] = torch.cuda.Event()
+        evs[k].record(stream)
+    stream.synchronize()
+    return out
+
+
+def to_host(t, dtype, shape):
+    """uint8 tensor -> host ndarray of ``dtype`` / ``shape`` (the mode's only D2H)."""
+    import torch
+    dtype = np.dtype(dtype)
+    if t.device.type != "cuda":
+        return t.numpy().view(dtype).reshape(shape)
+    n = t.numel()
+    stream = torch.cuda.current_stream(t.device)
+    if n <= SMALL:
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        if n:
+            host.copy_(t, non_blocking=True)
+            stream.synchronize()
+        return host.numpy().view(dtype).reshape(shape)
+    out = np.empty(n, dtype=np.uint8)
+    bufs = [torch.empty(CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    evs = [torch.cuda.Event(), torch.cuda.Event()]
+    starts = list(range(0, n, CHUNK))
+    # keep one DMA in flight ahead of the host copy out of the previous chunk
+    for i, lo in enumerate(starts):
+        hi = min(n, lo + CHUNK)
+        k = i % 2
+        bufs[k][:hi - lo].copy_(t[lo:hi], non_blocking=True)
+        evs[k].record(stream)
+        if i > 0:
+            plo = starts[i - 1]
+            phi = min(n, plo + CHUNK)
+            evs[1 - k].synchronize()
+            _par_copy(out[plo:phi], bufs[1 - k].numpy()[:phi - plo])
+    lo = starts[-1]
+    evs[(len(starts) - 1) % 2].synchronize()
+    _par_copy(out[lo:n], bufs[(len(starts) - 1) % 2].numpy()[:n - lo])
+    return out.view(dtype).reshape(shape)
