@@ -108,6 +108,9 @@ template <> struct Acc<M_MEAN> {
   int64_t n;
   __device__ void init() { K = 0; S1 = 0; S1b = 0; n = 0; }
   __device__ void first(double x) { K = x; S1 = 0; S1b = 0; n = 1; }
+  __device__ void pivot(double k) { K = k; S1 = 0; S1b = 0; n = 0; }
+  __device__ double s1() const { return S1 + S1b; }
+  __device__ double s2() const { return 0.0; }
   __device__ void add(double x) { S1 += x - K; ++n; }
   __device__ void add2(double x, double y) { S1 += x - K; S1b += y - K; n += 2; }
   __device__ double mean() const { return n ? K + (S1 + S1b) / (double)n : 0.0; }
@@ -119,6 +122,9 @@ template <> struct Acc<M_MOM> {
   int64_t n;
   __device__ void init() { K = 0; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 0; }
   __device__ void first(double x) { K = x; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 1; }
+  __device__ void pivot(double k) { K = k; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 0; }
+  __device__ double s1() const { return S1 + S1b; }
+  __device__ double s2() const { return S2 + S2b; }
   __device__ void add(double x) {
     const double dx = x - K;
     S1 += dx;
@@ -141,6 +147,14 @@ template <> struct Acc<M_MOM> {
     return v > 0.0 ? v : 0.0;
   }
 };
+
+// (n, K, S1, S2) of pivot-shifted sums -> mean, M2
+__device__ __forceinline__ void from_sums(double n, double K, double s1, double s2, double &mean,
+                                          double &m2) {
+  mean = n > 0.0 ? K + s1 / n : 0.0;
+  const double v = n > 0.0 ? s2 - s1 * (s1 / n) : 0.0;
+  m2 = v > 0.0 ? v : 0.0;
+}
 
 // Chan et al. pairwise combination of (n, mean, M2) -- statcounter.py:85-96
 // in its exact form (no 10x heuristic needed in float64).
@@ -252,13 +266,12 @@ __global__ void __launch_bounds__(kThreads)
     const T *base = src + ((int64_t)o * d.R) * d.I + col0;
     int64_t r = r_lo + ph;
     if (MODE == M_MEAN || MODE == M_MOM) {
-      if (r < r_hi) {
-        T v[VEC];
-        vload_nt<T, VEC>(base + r * d.I, v);
+      // one pivot per column for every row phase of the block (the chunk's
+      // first row): the phases then combine by plain sums, no divisions
+      T k0[VEC];
+      vload<T, VEC>(base + r_lo * d.I, k0);
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[k].first(to_f64(v[k]));
-        r += nph;
-      }
+      for (int k = 0; k < VEC; ++k) acc[k].pivot(to_f64(k0[k]));
     }
     for (; r + 3 * nph < r_hi; r += 4 * nph) {
       T v0[VEC], v1[VEC], v2[VEC], v3[VEC];
@@ -298,10 +311,11 @@ __global__ void __launch_bounds__(kThreads)
     const int64_t span = r_hi - r_lo - ph;
     n_own = span > 0 ? (double)((span + nph - 1) / nph) : 0.0;
   }
+  // mean / moment modes carry the shared-pivot sums (S1, S2) until the end
   double m_[VEC], q_[VEC];
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
-    if (MODE == M_MEAN || MODE == M_MOM) { m_[k] = acc[k].mean(); q_[k] = acc[k].m2(); }
+    if (MODE == M_MEAN || MODE == M_MOM) { m_[k] = acc[k].s1(); q_[k] = acc[k].s2(); }
     else if (MODE == M_FSUM) { m_[k] = fs[k]; q_[k] = 0.0; }
     else { m_[k] = __builtin_bit_cast(double, us[k]); q_[k] = 0.0; }
   }
@@ -322,9 +336,8 @@ __global__ void __launch_bounds__(kThreads)
         for (int k = 0; k < VEC; ++k) {
           const double mb = sm0[other * VEC + k];
           if (MODE == M_MEAN || MODE == M_MOM) {
-            double na = n0, ma = m_[k], qa = q_[k];
-            chan(na, ma, qa, nb, mb, (MODE == M_MOM) ? sm1[other * VEC + k] : 0.0, MODE == M_MOM);
-            m_[k] = ma; q_[k] = qa;
+            m_[k] += mb;
+            if (MODE == M_MOM) q_[k] += sm1[other * VEC + k];
           } else if (MODE == M_FSUM) {
             m_[k] += mb;
           } else {
@@ -342,6 +355,7 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t plane = d.O * d.I;
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
+    if (MODE == M_MEAN || MODE == M_MOM) from_sums(ntot, acc[k].K, m_[k], q_[k], m_[k], q_[k]);
     const int64_t e = (int64_t)o * d.I + col0 + k;
     const int64_t idx = sk.final_out ? e : (c * plane + e);
     emit<MODE>(sk, idx, ntot, m_[k], q_[k], __builtin_bit_cast(uint64_t, m_[k]));
@@ -374,19 +388,9 @@ __global__ void __launch_bounds__(kThreads)
   uint64_t us = bident<T, MODE>();
   int64_t j = r_lo + (int64_t)lane * VEC;
   const int64_t stride = 64 * VEC;
-  if ((MODE == M_MEAN || MODE == M_MOM) && j < r_hi) {
-    if (j + VEC <= r_hi) {
-      T v[VEC];
-      vload_nt<T, VEC>(row + j, v);
-      acc.first(to_f64(v[0]));
-#pragma unroll
-      for (int k = 1; k < VEC; ++k) acc.add(to_f64(v[k]));
-    } else {
-      acc.first(to_f64(row[j]));
-      for (int64_t k = j + 1; k < r_hi; ++k) acc.add(to_f64(row[k]));
-    }
-    j += stride;
-  }
+  // one pivot for the whole (row, chunk) -- its first element -- so the
+  // 64 lanes combine by plain sums (no per-step division, see butterfly)
+  if (MODE == M_MEAN || MODE == M_MOM) acc.pivot(to_f64(row[r_lo]));
   // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
   for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
     T v[kRowsUnroll][VEC];
@@ -426,24 +430,19 @@ __global__ void __launch_bounds__(kThreads)
     }
   }
 
-  // wave combination (butterfly, fixed order -> deterministic)
-  double n = (double)acc.n, m = acc.mean(), q = acc.m2();
+  // wave combination (butterfly, fixed order -> deterministic): shared
+  // pivot, so the lanes' (S1, S2) simply add; the element count is known
+  double m = acc.s1(), q = acc.s2();
   if (MODE == M_FSUM) m = fs;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     if (MODE == M_MEAN || MODE == M_MOM) {
-      const double nb = __shfl_xor(n, off);
       const double mb = __shfl_xor(m, off);
       const double qb = (MODE == M_MOM) ? __shfl_xor(q, off) : 0.0;
-      // lower lane keeps (self, partner) order, upper lane (partner, self):
-      // both compute the same ordered combination of the two halves.
-      if (lane & off) {
-        double na = nb, ma = mb, qa = qb;
-        chan(na, ma, qa, n, m, q, MODE == M_MOM);
-        n = na; m = ma; q = qa;
-      } else {
-        chan(n, m, q, nb, mb, qb, MODE == M_MOM);
-      }
+      // lower lane adds (self + partner), upper lane (partner + self):
+      // the same ordered sum on both sides of every butterfly step
+      m = (lane & off) ? (mb + m) : (m + mb);
+      if (MODE == M_MOM) q = (lane & off) ? (qb + q) : (q + qb);
     } else if (MODE == M_FSUM) {
       const double mb = __shfl_xor(m, off);
       m = (lane & off) ? (mb + m) : (m + mb);
@@ -454,6 +453,7 @@ __global__ void __launch_bounds__(kThreads)
   }
   if (lane != 0) return;
   const double ntot = (double)(r_hi - r_lo);
+  if (MODE == M_MEAN || MODE == M_MOM) from_sums(ntot, acc.K, m, q, m, q);
   const int64_t e = (int64_t)o;
   const int64_t idx = sk.final_out ? e : (c * d.O + e);
   emit<MODE>(sk, idx, ntot, m, q, us);

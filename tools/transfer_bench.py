@@ -3,13 +3,16 @@
     python tools/transfer_bench.py [--mb 2000]
 """
 import argparse
+import os
+import sys
 import time
 
 import numpy as np
 import torch
 
-import bolt_amd as bolt
-from bolt_amd.mi355x.transfer import to_device, to_host
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bolt_amd as bolt  # noqa: E402
+from bolt_amd.mi355x.transfer import to_device, to_host  # noqa: E402
 
 
 def best(f, reps=3):
