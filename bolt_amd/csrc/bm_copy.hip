@@ -513,8 +513,8 @@ extern "C" int bm_copy_strided(const void *src_, void *dst_, int ndim, const int
   }
   std::vector<Dim> dims;
   for (int k = 0; k < ndim; ++k) {
-    if (shape[k] < 0 || src_strides[k] < 0 || dst_strides[k] < 0) {
-      bm_set_error("bm_copy_strided: negative shape/stride at dim %d", k);
+    if (shape[k] < 0 || dst_strides[k] < 0) {  // source strides may be negative (reversed slices)
+      bm_set_error("bm_copy_strided: negative shape / destination stride at dim %d", k);
       return BM_E_ARG;
     }
     if (shape[k] == 0) return BM_OK;  // empty: nothing to move

@@ -74,6 +74,21 @@ class HipBackend(object):
                                        _lib.i64_array(shape), _lib.i32_array(perm), int(es),
                                        self._stream(src)), "bm_permute")
 
+    def gather_rows(self, src, src_off, dst, dst_off, n_outer, src_rows, row_bytes, idx):
+        """dst[a, j, :] = src[a, idx[j], :] (byte offsets; idx a host int64 array, bounds-checked)."""
+        import torch
+        idx = np.ascontiguousarray(idx, dtype=np.int64).reshape(-1)
+        if idx.size == 0 or n_outer == 0:
+            return
+        if idx.min() < 0 or idx.max() >= src_rows:
+            raise IndexError("gather index out of range [0, %d)" % src_rows)
+        didx = torch.from_numpy(idx).to(src.device, non_blocking=False)
+        _lib.check(self.lib.bm_gather_rows(self._ptr(src, src_off), self._ptr(dst, dst_off), int(n_outer),
+                                           int(src_rows), int(row_bytes), ctypes.c_void_p(didx.data_ptr()),
+                                           int(idx.size), self._stream(src)), "bm_gather_rows")
+        # the caching allocator must not hand the index buffer out before the kernel has read it
+        didx.record_stream(torch.cuda.current_stream(src.device))
+
     def _workspace(self, stat, code, O, R, I, device):
         import torch
         n = ctypes.c_size_t(0)

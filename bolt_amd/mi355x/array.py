@@ -24,7 +24,7 @@ from bolt_amd.mi355x import _lib
 from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
 from bolt_amd.mi355x.context import contiguous_strides, local_shape
-from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, _empty
+from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, redistribute_rows, select_sharded, _empty
 from bolt_amd.mi355x.transfer import to_device, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
@@ -282,6 +282,76 @@ class BoltArrayMI355X(BoltArray):
         p[axis2] = axis1
         return self.transpose(p)
 
+    # ------------------------------------------------------------ indexing
+    def __getitem__(self, index):
+        """Index with ints, slices and lists (array.py:595-676).
+
+        Same normalisation, bounds errors, result shape/split and element
+        order as the reference (indexing.py): basic selections are one
+        strided copy, list selections one gather kernel; across GPUs rows
+        move with one all-to-all.  Int axes are squeezed out; an all-int
+        index returns a scalar.
+        """
+        from bolt_amd.mi355x import indexing
+        index, int_locs, kind = indexing.normalize(index, self._shape)
+        es = self._dtype.itemsize
+        if kind == 'basic':
+            starts = [s.start for s in index]
+            steps = [s.step for s in index]
+            shape = tuple(int(np.ceil((s.stop - s.start) / float(s.step))) for s in index)
+            data = select_sharded(self._ctx, self._backend, self._data, self._shape, starts, steps, shape, es)
+            result = self._like(data, shape, self._split)
+        elif kind == 'advanced':
+            pts, shape = indexing.advanced_points(index, self._shape, self._split)
+            if len(shape) == 0:
+                raise ValueError("0-d index arrays are not supported")
+            out_upr = int(np.prod(shape[1:], dtype=np.int64))
+            data = indexing.gather_units_sharded(self._ctx, self._backend, self._data, self._shape[0], es,
+                                                 int(np.prod(self._shape[1:], dtype=np.int64)), pts,
+                                                 shape[0], out_upr)
+            result = self._like(data, shape, len(shape))
+        else:
+            loc, idx = indexing.mixed_take(index, self._shape, self._split)
+            data = indexing.take_sharded(self._ctx, self._backend, self._data, self._shape, es, loc, idx)
+            newshape = list(self._shape)
+            newshape[loc] = len(idx)
+            taken = self._like(data, tuple(newshape), self._split)
+            rest = list(index)
+            rest[loc] = slice(0, None, None)
+            result = taken[tuple(rest)]
+        if len(int_locs) == self.ndim:
+            return result.toarray().reshape(())[()]
+        return result.squeeze(tuple(int_locs)) if int_locs else result
+
+    def squeeze(self, axis=None):
+        """Drop singleton axes (array.py:879-918); the data does not move on one
+        GPU, and re-slabs across GPUs when the leading axis goes away."""
+        if not any(d == 1 for d in self._shape):
+            return self
+        if axis is None:
+            drop = [i for i, d in enumerate(self._shape) if d == 1]
+        elif isinstance(axis, int):
+            drop = [axis]
+        elif isinstance(axis, tuple):
+            drop = [int(a) for a in axis]
+        else:
+            raise ValueError("an integer or tuple is required for the axis")
+        if any(self._shape[i] > 1 for i in drop):
+            raise ValueError("cannot select an axis to squeeze out which has size greater than one")
+        if not drop:
+            return self
+        shape = tuple(d for i, d in enumerate(self._shape) if i not in drop)
+        split = len([d for d in range(self._split) if d not in drop])
+        data = self._data
+        if 0 in drop and self._ctx.world_size > 1:
+            # the leading axis goes: re-slab on the new one (a 0-d result lives on rank 0)
+            es = self._dtype.itemsize
+            new_rows = shape[0] if shape else 1
+            new_rowbytes = int(np.prod(shape[1:], dtype=np.int64)) * es if shape else es
+            data = redistribute_rows(self._ctx, data, self._shape[0],
+                                     int(np.prod(self._shape[1:], dtype=np.int64)) * es, new_rows, new_rowbytes)
+        return self._like(data, shape, split)
+
     # ---------------------------------------------------------- statistics
     def _reduced(self, axis, stat):
         """Device reduction of ``axis`` -> host ndarray with the kept axes (ascending).
@@ -425,7 +495,8 @@ class BoltArrayMI355X(BoltArray):
         if ctx.world_size == 1:
             return self._data
         rowbytes = int(np.prod(self._shape[1:], dtype=np.int64)) * self._dtype.itemsize
-        sizes = [(hi - lo) * rowbytes for lo, hi in ctx.bounds(self._shape[0])]
+        rows = self._shape[0] if self._shape else 1  # a 0-d array lives on rank 0
+        sizes = [(hi - lo) * rowbytes for lo, hi in ctx.bounds(rows)]
         return all_gather_bytes(ctx, self._data, sizes)
 
     def toarray(self):

@@ -69,6 +69,8 @@ class MI355XContext(object):
 
 
 def local_shape(ctx, shape):
+    if len(shape) == 0:  # a 0-d array (everything squeezed out) lives on rank 0
+        return () if ctx.rank == 0 else (0,)
     lo, hi = ctx.local_bounds(shape[0])
     return (hi - lo,) + tuple(shape[1:])
 

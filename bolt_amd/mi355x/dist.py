@@ -62,6 +62,8 @@ def _wide(t, sizes, unit):
     if unit not in (4, 8):  # (gloo has no 16-bit collectives)
         unit = 1
     dt = {8: torch.int64, 4: torch.int32, 1: torch.uint8}[unit]
+    if t.numel() == 0:  # an empty slab may carry any stride
+        return torch.empty(0, dtype=dt, device=t.device), [0 for _ in sizes]
     return t.view(dt), [int(s) // unit for s in sizes]
 
 
@@ -209,6 +211,80 @@ def _unpack(backend, pending, out, tstr, j, es):
                                  contiguous_strides(bshape), tstr, es)
         off += nb
     del send
+
+
+def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es):
+    """This rank's slab of x[start_k :: step_k] (basic slicing) for a sharded x.
+
+    Output row i of the leading axis is input row starts[0] + i*steps[0].  On
+    one GPU this is a single strided copy; across GPUs each rank packs, for
+    every destination, the selected rows it holds (they form one run of
+    output rows), one all-to-all moves them, and they land in order.
+    """
+    shape = tuple(int(x) for x in shape)
+    out_shape = tuple(int(x) for x in out_shape)
+    in_b = ctx.bounds(shape[0])
+    out_b = ctx.bounds(out_shape[0])
+    r = ctx.rank
+    mlo, mhi = in_b[r]
+    sin = contiguous_strides((mhi - mlo,) + shape[1:])
+    sstr = [sin[k] * steps[k] for k in range(len(shape))]
+    inner_off = sum(starts[k] * sin[k] for k in range(1, len(shape)))
+    lo, hi = out_b[r]
+    loc_out = (hi - lo,) + out_shape[1:]
+    out = _empty(int(np.prod(loc_out)) * es, data.device)
+    ostr = contiguous_strides(loc_out)
+
+    def rows_from(src_lo, src_hi, q_lo, q_hi):
+        """Output rows i in [q_lo, q_hi) whose input row lies in [src_lo, src_hi)."""
+        s0, st = starts[0], steps[0]
+        ilo, ihi = q_lo, q_hi
+        if st > 0:
+            ilo = max(ilo, -((s0 - src_lo) // st))          # ceil((src_lo - s0) / st)
+            ihi = min(ihi, -((s0 - src_hi) // st))
+        else:
+            ilo = max(ilo, (s0 - src_hi) // (-st) + 1)        # s0 + i*st <= src_hi - 1
+            ihi = min(ihi, (s0 - src_lo) // (-st) + 1)        # s0 + i*st >= src_lo
+        return ilo, max(ilo, ihi)
+
+    def copy_rows(i0, i1, dst, dst_off, dst_strides):
+        n = i1 - i0
+        if n <= 0:
+            return 0
+        src_row = starts[0] + i0 * steps[0] - mlo
+        shp = (n,) + out_shape[1:]
+        backend.copy_strided(data, (src_row * sin[0] + inner_off) * es, dst, dst_off, shp, sstr,
+                             dst_strides, es)
+        return int(np.prod(shp)) * es
+
+    if ctx.world_size == 1:
+        copy_rows(0, out_shape[0], out, 0, ostr)
+        return out
+    send_sizes, blocks = [], []
+    for q in range(ctx.world_size):
+        qlo, qhi = out_b[q]
+        i0, i1 = rows_from(mlo, mhi, qlo, qhi)
+        blocks.append((i0, i1))
+        send_sizes.append((i1 - i0) * int(np.prod(out_shape[1:])) * es)
+    send = _empty(sum(send_sizes), data.device)
+    off = 0
+    for (i0, i1), nb in zip(blocks, send_sizes):
+        if nb:
+            copy_rows(i0, i1, send, off, contiguous_strides((i1 - i0,) + out_shape[1:]))
+        off += nb
+    recv_sizes, rblocks = [], []
+    for s_ in range(ctx.world_size):
+        slo, shi = in_b[s_]
+        i0, i1 = rows_from(slo, shi, lo, hi)
+        rblocks.append((i0, i1))
+        recv_sizes.append((i1 - i0) * int(np.prod(out_shape[1:])) * es)
+    recv = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(es))
+    off = 0
+    for (i0, i1), nb in zip(rblocks, recv_sizes):
+        if nb:
+            out[(i0 - lo) * ostr[0] * es:(i1 - lo) * ostr[0] * es].copy_(recv[off:off + nb])
+        off += nb
+    return out
 
 
 def redistribute_rows(ctx, data, old_rows, old_rowbytes, new_rows, new_rowbytes):

@@ -43,6 +43,40 @@ def allclose(a, b):
     return (a.shape == b.shape) and np.allclose(a, b)
 
 
+def slicify(slc, dim):
+    """A slice with explicit start/stop/step inside [0, dim] (bolt/utils.py:105-147).
+
+    Start and stop are made non-negative; a negative step that runs past the
+    front keeps stop = -1 (the one negative value, handled by the caller);
+    an int i becomes slice(i, i+1, 1).
+    """
+    if isinstance(slc, slice):
+        start = 0 if slc.start is None else slc.start
+        stop = dim if slc.stop is None else slc.stop
+        step = 1 if slc.step is None else slc.step
+        if start < 0:
+            start += dim
+        if stop < 0:
+            stop += dim
+        if step > 0:
+            if start < 0:
+                start = 0
+            if stop > dim:
+                stop = dim
+        else:
+            if stop < 0:
+                stop = -1
+            if start > dim:
+                start = dim - 1
+        return slice(start, stop, step)
+    elif isinstance(slc, int):
+        if slc < 0:
+            slc += dim
+        return slice(slc, slc + 1, 1)
+    else:
+        raise ValueError("Type for slice %s not recongized" % type(slc))
+
+
 def istransposeable(new, old):
     """Validate a proposed permutation: length, repeats, bounds (bolt/utils.py:149-172)."""
     new, old = tupleize(new), tupleize(old)

@@ -81,9 +81,12 @@ int bm_device_cus(void);
  *   - values_to_keys flatMap(_extract)      bolt/spark/chunk.py:291-347
  *   - Keys.transpose / Values.transpose     bolt/spark/shapes.py:66-89, :136-159
  *   - the multi-GPU swap's pack and unpack around the all-to-all
+ *   - basic indexing, BoltArraySpark._getbasic  bolt/spark/array.py:480-512
  * Element i = (i_0..i_{n-1}) is read at src + sum(i_k*src_strides[k]) and
- * written at dst + sum(i_k*dst_strides[k]) (strides in elements, may be
- * any non-negative values; dst must not overlap itself or src).
+ * written at dst + sum(i_k*dst_strides[k]) (strides in elements; source
+ * strides may be negative -- a reversed slice, BoltArraySpark.__getitem__
+ * array.py:480-676 -- destination strides are >= 0; dst must not overlap
+ * itself or src).
  * elem_bytes: any positive size (1/2/4/8/16 are native; others are moved
  * as bytes).  Data is moved bit-exactly.  ndim <= 24.
  */
@@ -100,6 +103,19 @@ int bm_copy_strided(const void *src, void *dst, int ndim, const int64_t *shape,
  */
 int bm_permute(const void *src, void *dst, int ndim, const int64_t *shape,
                const int32_t *perm, int elem_bytes, void *stream);
+
+/*
+ * bm_gather_rows -- dst[a, j, :] = src[a, idx[j], :] for a C-contiguous src
+ * viewed as [n_outer][src_rows][row_bytes]; dst is [n_outer][n_idx][row_bytes].
+ * idx is a DEVICE array of n_idx int64 row numbers in [0, src_rows) (the host
+ * checks bounds, as BoltArraySpark.__getitem__ does, array.py:652-659).
+ * The non-strided selections of __getitem__ (bolt/spark/array.py:514-593):
+ *   _getmixed    one index list on one axis (x.take(idx, axis)),
+ *   _getadvanced one list per axis -> a point gather (row = one element).
+ * Bit-exact for every dtype.
+ */
+int bm_gather_rows(const void *src, void *dst, int64_t n_outer, int64_t src_rows,
+                   int64_t row_bytes, const int64_t *idx, int64_t n_idx, void *stream);
 
 /*
  * Reductions over a C-contiguous array viewed as [O][R][I]: the middle axis

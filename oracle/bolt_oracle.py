@@ -451,6 +451,154 @@ def min_(rs, axis=None, keepdims=False):
     return reduce_(rs, np.minimum, axis, keepdims)
 
 
+# ---------------------------------------------------------------- indexing
+def slicify(slc, dim):
+    """bolt/utils.py:105-147: explicit start/stop/step; stop -1 marks a negative
+    step running past the front; an int i is slice(i, i+1, 1)."""
+    if isinstance(slc, slice):
+        start = 0 if slc.start is None else slc.start
+        stop = dim if slc.stop is None else slc.stop
+        step = 1 if slc.step is None else slc.step
+        start = start + dim if start < 0 else start
+        stop = stop + dim if stop < 0 else stop
+        if step > 0:
+            start, stop = max(start, 0), min(stop, dim)
+        else:
+            stop = -1 if stop < 0 else stop
+            start = dim - 1 if start > dim else start
+        return slice(start, stop, step)
+    if isinstance(slc, int):
+        return slice(slc + dim if slc < 0 else slc, (slc + dim if slc < 0 else slc) + 1, 1)
+    raise ValueError("Type for slice %s not recongized" % type(slc))
+
+
+def _getbasic(rs, index):
+    """array.py:480-512 (value index as a tuple)."""
+    ks, vs = index[:rs.split], index[rs.split:]
+
+    def keep(key):
+        for k, s in zip(key, ks):
+            inside = (s.start <= k < s.stop) if s.step > 0 else (s.stop < k <= s.start)
+            if not inside or (k - s.start) % s.step:
+                return False
+        return True
+
+    vt = tuple(s if s.stop != -1 else slice(s.start, None, s.step) for s in vs)
+    parts = [[(tuple((k - s.start) // s.step for k, s in zip(key, ks)), v[vt] if vs else v)
+              for key, v in p if keep(key)] for p in rs.parts]
+    shape = tuple(int(np.ceil((s.stop - s.start) / float(s.step))) for s in index)
+    return RecSet(parts, shape, rs.split, rs.dtype)
+
+
+def _getadvanced(rs, index):
+    """array.py:514-559: listed keys in record order, each expanded into the
+    value positions of its (last consecutive) group, renumbered in order."""
+    index = [np.asarray(i) for i in index]
+    ishape = index[0].shape
+    if not all(i.shape == ishape for i in index):
+        raise ValueError("shape mismatch: indexing arrays could not be broadcast together")
+    flat = []
+    for i, d in zip(index, rs.shape):
+        if not all(np.asarray(v).dtype == int for v in i):
+            raise ValueError("indices must be integers")
+        if np.any(i >= d):
+            raise ValueError("indices out of bounds for axis with size %s" % d)
+        flat.append(i.flatten())
+    keys = [tuple(int(v) for v in t) for t in zip(*flat[:rs.split])]
+    vals = [tuple(int(v) for v in t) for t in zip(*flat[rs.split:])]
+    groups = {}
+    for pos, (k, v) in enumerate(zip(keys, vals) if vals else [(k, None) for k in keys]):
+        if pos == 0 or keys[pos - 1] != k:
+            groups[k] = []
+        groups[k].append(v)
+    out = []
+    for key, v in rs.records():
+        if key in groups:
+            out.extend([v[t] for t in groups[key]] if vals else [v])
+    recs = [(tuple(int(i) for i in np.unravel_index(n, ishape)), val) for n, val in enumerate(out)]
+    return RecSet([recs], ishape, len(ishape), rs.dtype)
+
+
+def _getmixed(rs, index):
+    """array.py:561-593 (value index as a tuple): the listed axis first, then
+    the basic selection through getitem again, as the reference composes it."""
+    loc = [i for i, x in enumerate(index) if isinstance(x, np.ndarray)][0]
+    idx = list(index[loc])
+    if isinstance(idx[0], (tuple, list, np.ndarray)):
+        raise ValueError("When mixing basic and advanced indexing, advanced index must be one-dimensional")
+    if loc < rs.split:
+        parts = [[(key[:loc] + (idx.index(key[loc]),) + key[loc + 1:], v) for key, v in p if key[loc] in idx]
+                 for p in rs.parts]
+    else:
+        vt = [slice(None)] * (len(rs.shape) - rs.split)
+        vt[loc - rs.split] = idx
+        parts = [[(key, v[tuple(vt)]) for key, v in p] for p in rs.parts]
+    shape = list(rs.shape)
+    shape[loc] = len(idx)
+    rest = list(index)
+    rest[loc] = slice(0, None, None)
+    return getitem(RecSet(parts, shape, rs.split, rs.dtype), tuple(rest))
+
+
+def squeeze(rs, axis=None):
+    """BoltArraySpark.squeeze (array.py:879-918)."""
+    if not any(d == 1 for d in rs.shape):
+        return rs
+    if axis is None:
+        drop = [i for i, d in enumerate(rs.shape) if d == 1]
+    elif isinstance(axis, int):
+        drop = [axis]
+    elif isinstance(axis, tuple):
+        drop = list(axis)
+    else:
+        raise ValueError("an integer or tuple is required for the axis")
+    if any(rs.shape[i] > 1 for i in drop):
+        raise ValueError("cannot select an axis to squeeze out which has size greater than one")
+    vdrop = tuple(d - rs.split for d in drop if d >= rs.split)
+    parts = [[(tuple(k for i, k in enumerate(key) if i not in drop), v.squeeze(vdrop) if vdrop else v)
+              for key, v in p] for p in rs.parts]
+    shape = tuple(s for i, s in enumerate(rs.shape) if i not in drop)
+    split = len([d for d in range(rs.split) if d not in drop])
+    return RecSet(parts, shape, split, rs.dtype)
+
+
+def getitem(rs, index):
+    """BoltArraySpark.__getitem__ (array.py:595-676)."""
+    index = list(index) if isinstance(index, tuple) else [index]
+    int_locs = [i for i, x in enumerate(index) if isinstance(x, int)]
+    nd = len(rs.shape)
+    if len(index) > nd:
+        raise ValueError("Too many indices for array")
+    if not all(isinstance(i, (slice, int, list, tuple, np.ndarray)) for i in index):
+        raise ValueError("Each index must either be a slice, int, list, set, or ndarray")
+    index += [slice(0, None, None)] * (nd - len(index))
+    for n, idx in enumerate(index):
+        size = rs.shape[n]
+        if isinstance(idx, (slice, int)):
+            s = slicify(idx, size)
+            lo, hi = (s.start, s.stop) if s.step > 0 else (s.stop, s.start)
+            if lo > size - 1 or hi < 1 or lo >= hi:
+                raise ValueError("Index %s in dimension %d would produce an empty dimension" % (idx, n))
+            index[n] = s
+        else:
+            a = np.array(idx)
+            a[np.where(a < 0)] += size
+            if a.min() < 0 or a.max() > size - 1:
+                raise ValueError("Index %s out of bounds in dimension %d" % (idx, n))
+            index[n] = a
+    if all(isinstance(i, slice) for i in index):
+        out = _getbasic(rs, index)
+    elif all(isinstance(i, np.ndarray) for i in index):
+        out = _getadvanced(rs, index)
+    elif sum(isinstance(i, np.ndarray) for i in index) == 1:
+        out = _getmixed(rs, index)
+    else:
+        raise NotImplementedError("only a single advanced index may be mixed with basic indices")
+    if len(int_locs) == nd:
+        return toarray(squeeze(out)).reshape(())[()]
+    return squeeze(out, tuple(int_locs))
+
+
 def repartition(rs, n):
     """Records in key order split into n contiguous partitions (parallelize's cut)."""
     recs = sorted(rs.records(), key=lambda kv: kv[0])

@@ -50,6 +50,16 @@ class CpuBackend(object):
         d = _view(_np(dst), dst_off, shape, dstrides, es)
         d[...] = s
 
+    def gather_rows(self, src, src_off, dst, dst_off, n_outer, src_rows, row_bytes, idx):
+        idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+        if idx.size == 0 or n_outer == 0:
+            return
+        if idx.min() < 0 or idx.max() >= src_rows:
+            raise IndexError("gather index out of range [0, %d)" % src_rows)
+        s = _np(src)[src_off:src_off + n_outer * src_rows * row_bytes].reshape(n_outer, src_rows, row_bytes)
+        d = _np(dst)[dst_off:dst_off + n_outer * idx.size * row_bytes].reshape(n_outer, idx.size, row_bytes)
+        d[...] = s[:, idx, :]
+
     def permute(self, src, shape, perm, es, dst):
         a = _np(src).view(np.dtype((np.void, es))).reshape(tuple(shape))
         out = _np(dst).view(np.dtype((np.void, es)))

@@ -10,6 +10,8 @@ fakerdd.py) with two shims for behaviour the reference relied on from old
 numpy:
   * ChunkedArray.removepad indexes with tuple(slices) (chunk.py:550 passes a
     list, which numpy >= 1.23 rejects);
+  * _getbasic / _getmixed index a value with tuple(slices) (array.py:508,
+    :584 pass lists);
   * after keys_to_values squeezes the all-keys singleton value axis
     (chunk.py:284-287) the padding and the stale trailing chunk id are
     trimmed, as numpy < 1.13's short boolean masks did.
@@ -32,6 +34,7 @@ collections.Iterable = collections.abc.Iterable  # bolt/utils.py:3 on Python >= 
 import numpy as np  # noqa: E402
 
 import bolt  # noqa: E402
+from bolt.spark.array import BoltArraySpark  # noqa: E402
 from bolt.spark.chunk import ChunkedArray  # noqa: E402
 from fakerdd import FakeContext  # noqa: E402
 from inputs import make_input  # noqa: E402
@@ -64,6 +67,62 @@ def _keys_to_values(self, axes, size=None):
 
 
 ChunkedArray.keys_to_values = _keys_to_values
+
+
+# BoltArraySpark._getbasic / _getmixed index a record's value with a LIST of
+# slices (array.py:508, :584), which numpy < 1.23 read as a tuple; numpy 2
+# raises IndexError.  Same logic, the value index passed as a tuple.
+def _getbasic(self, index):
+    ksl, vsl = index[:self.split], index[self.split:]
+
+    def keep(key):
+        for k, s in zip(key, ksl):
+            inside = (s.start <= k < s.stop) if s.step > 0 else (s.stop < k <= s.start)
+            if not (inside and np.mod(k - s.start, s.step) == 0):
+                return False
+        return True
+
+    def rekey(key):
+        return tuple([(k - s.start) / s.step for k, s in zip(key, ksl)])
+
+    picked = self._rdd.filter(lambda kv: keep(kv[0]))
+    if self._split == self.ndim:
+        rdd = picked.map(lambda kv: (rekey(kv[0]), kv[1]))
+    else:
+        vt = tuple(s if s.stop != -1 else slice(s.start, None, s.step) for s in vsl)
+        rdd = picked.map(lambda kv: (rekey(kv[0]), kv[1][vt]))
+    shape = tuple([int(np.ceil((s.stop - s.start) / float(s.step))) for s in index])
+    return rdd, shape, self.split
+
+
+def _getmixed(self, index):
+    loc = np.where([isinstance(i, (tuple, list, np.ndarray)) for i in index])[0][0]
+    idx = list(index[loc])
+    if isinstance(idx[0], (tuple, list, np.ndarray)):
+        raise ValueError("When mixing basic and advanced indexing, "
+                         "advanced index must be one-dimensional")
+    if loc < self.split:
+        def rekey(key):
+            key = list(key)
+            key[loc] = idx.index(key[loc])
+            return tuple(key)
+        rdd = self._rdd.filter(lambda kv: kv[0][loc] in idx).map(lambda kv: (rekey(kv[0]), kv[1]))
+    else:
+        vt = [slice(0, None, None) for _ in self.values.shape]
+        vt[loc - self.split] = idx
+        vt = tuple(vt)
+        rdd = self._rdd.map(lambda kv: (kv[0], kv[1][vt]))
+    newshape = list(self.shape)
+    newshape[loc] = len(idx)
+    b = self._constructor(rdd, shape=tuple(newshape)).__finalize__(self)
+    rest = index[:]
+    rest[loc] = slice(0, None, None)
+    b = b[tuple(rest)]
+    return b._rdd, b.shape, b.split
+
+
+BoltArraySpark._getbasic = _getbasic
+BoltArraySpark._getmixed = _getmixed
 
 
 # ---------------------------------------------------------------- cases
@@ -368,10 +427,103 @@ def gen_stat_errors():
         add(case)
 
 
+def enc_item(i):
+    if isinstance(i, slice):
+        return {"slice": [i.start, i.stop, i.step]}
+    if isinstance(i, np.ndarray):
+        return {"array": i.tolist()}
+    return i  # int or (nested) list
+
+
+def gen_getitem():
+    S = slice
+    x66 = spec((6, 6))
+    basic = [(S(0, 1), S(0, 1)), (S(0, 2), S(0, 2)), (S(0, 2), S(0, 3)), (S(0, 2), S(0, 3, 2)),
+             (S(None, 2), S(None, 2)), (S(1, None), S(1, None)), (S(5, 1, -1), S(5, 1, -1)),
+             (S(10, -10, -2), S(10, -10, -2)), (S(-5, -1), S(-5, -1)), (S(-1, -5, -2), S(-1, -5, -2)),
+             (S(None, None, -1), S(None, None, -1)), (S(None, None, -2), 3), (-1, S(None, None, -3)),
+             (S(2, 3),), S(1, 4), 2]
+    items = [(x66, ax, idx) for ax in ((0,), (0, 1)) for idx in basic]
+    x1010 = spec((10, 10, 3))
+    items += [(x1010, (0, 1), idx) for idx in [(S(0, 5, 2), S(0, 2)), (S(0, 5, 3), S(0, 2)), (S(0, 9, 3), S(0, 2)),
+                                               (S(9, None, -4), S(None, None, -2), S(2, 0, -1))]]
+    x23 = spec((2, 3))
+    ints = [(0, 0), (0, 1), (0, S(0, 1)), (1, 2), 0, [0], ([1], [2]), ([1], 2), (-1, -2), (1,), [-1],
+            ([1, 0], [0, 2]), ([0, 1, 1], [2, 0, 1])]
+    items += [(x23, ax, idx) for ax in ((0,), (0, 1)) for idx in ints]
+    x334 = spec((3, 3, 4))
+    lists = [([0, 1], [0, 1], [0, 2]), ([0, 1], [0, 2], [0, 3]), ([0, 1, 2], [0, 2, 1], [0, 3, 1]),
+             ([[0, 0], [1, 1]], [[0, 2], [0, 2]], [[0, 3], [0, 3]]),
+             ([2, 0, 1], [0, 1, 2], [1, 1, 1]), ([0, 0, 1], [2, 1, 0], [0, 1, 2]), ([0, 1, 0], [2, 1, 0], [0, 1, 2]),
+             ([-1, 0], [1, -3], [-4, 3]), (np.array([1, 2]), np.array([0, 0]), np.array([3, 2])),
+             ([0, 1], [0, 1]), ([0, 3], [0, 1], [0, 1]), ([0, 1], [0, 1, 2], [0, 1])]
+    items += [(x334, ax, idx) for ax in ((0,), (0, 1), (0, 1, 2)) for idx in lists]
+    x4 = spec((4, 4, 4, 4), "float32", "normal", 21)
+    i, s2 = [0, 1], S(1, 3)
+    mixed = [(i, S(None), S(None), S(None)), (i, s2, s2, s2), (S(None), S(None), i, S(None)), (s2, s2, i, s2),
+             ([1], S(None), S(None), S(None)), (S(None), S(None), [1], S(None)),
+             ([[0, 1], [1, 0]], S(None), S(None), S(None)), ([2, 0], S(None), S(None), S(None)),
+             (S(None), [3, 1, 1], S(None), S(None)), (S(None), S(None), [3, 1, 1], S(None)),
+             (S(None), S(None), S(None), [2, 0, 3]), ([0, 1], S(None, None, -1)), ([3, 1], 2, S(None), 1),
+             (1, [2, 0], S(0, 4, 2)), (S(None), S(None), [-1, 0], -1)]
+    items += [(x4, ax, idx) for ax in ((0,), (0, 1), (0, 1, 2)) for idx in mixed]
+    x5 = spec((5,))
+    items += [(x5, (0,), idx) for idx in [5, -6, [1, 5], S(3, 2), S(5, None), S(-6, 0), S(0, 5, -1),
+                                          (0, 0), 4, -5, [4, 0, 0], S(None, None, -1)]]
+    xb = spec((7, 5, 6), "uint16", "ints", 22)
+    for ax, npart in [((0,), 3), ((0, 1), 4), ((1,), 2)]:
+        for idx in [(S(6, 0, -2), S(None, None, -1), S(1, 5, 3)), (S(1, 6, 2), 4), (3, S(None), [5, 0, 2]),
+                    ([6, 2, 3], S(4, None, -2)), ([0, 6], [4, 1], [5, 0]), (-2,), (S(None), S(None), 0)]:
+            items.append((xb, ax, idx, npart))
+    for it in items:
+        s, ax, idx = it[:3]
+        npart = it[3] if len(it) > 3 else None
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=ax, npartitions=npart)
+        enc = {"tuple": [enc_item(j) for j in idx]} if isinstance(idx, tuple) else {"item": enc_item(idx)}
+        case = {"op": "getitem", "input": s, "axis": list(ax), "npartitions": npart, "index": enc}
+        r = run(lambda: b[idx], case)
+        if r is None and "raises" in case:
+            add(case)
+            continue
+        if isinstance(r, BoltArraySpark):
+            arr = run(lambda: r.toarray(), case)
+            if arr is None:
+                case["collect_raises"] = case.pop("raises")
+                case.update(shape=list(r.shape), split=r.split)
+                add(case)
+                continue
+            case.update(kind="array", shape=list(r.shape), split=r.split)
+            srt = _sorted_array(r)
+            if srt.tobytes() != arr.tobytes():  # toarray skips the sort
+                case["toarray_unsorted"] = True
+                add(case, out=arr, out_sorted=srt)
+            else:
+                add(case, out=arr)
+        else:
+            case.update(kind="scalar", result_type=type(r).__name__)
+            add(case, out=np.asarray(r))
+    for shp, ax, sq in [((1, 2, 1, 4), (0,), [None, (0, 2), 0, 2]), ((1, 2, 1, 4), (0, 1), [None, (0, 2), 0, 2]),
+                        ((1, 1, 1, 1), (0, 1), [None, (1, 3)]), ((3, 1, 2), (0, 1), [1, None, 0, (1,)]),
+                        ((2, 1, 1), (0, 1, 2), [None, 2])]:
+        s = spec(shp, "float64", "normal", 23)
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=ax)
+        for q in sq:
+            case = {"op": "squeeze", "input": s, "axis": list(ax), "npartitions": None,
+                    "squeeze": list(q) if isinstance(q, tuple) else q}
+            r = run(lambda: b.squeeze(q), case)
+            if r is None and "raises" in case:
+                add(case)
+                continue
+            case.update(shape=list(r.shape), split=r.split)
+            add(case, out=r.toarray())
+
+
 if __name__ == "__main__":
     sc = FakeContext(2)
     for g in (gen_construct, gen_swap, gen_transpose, gen_chunk, gen_moves, gen_getplan, gen_stats,
-              gen_stat_errors):
+              gen_stat_errors, gen_getitem):
         try:
             g()
         except Exception:

@@ -87,3 +87,18 @@ def stat_close(got, ref, truth, out_dtype, x):
     ok2 = np.abs(got - truth) <= np.abs(ref - truth) + 2 * eps * np.abs(truth) + eps * rtol * scale
     both_nan = np.isnan(got) & np.isnan(ref)
     return bool(np.all(ok1 | ok2 | both_nan))
+
+
+def _dec_item(i):
+    if isinstance(i, dict) and "slice" in i:
+        return slice(*i["slice"])
+    if isinstance(i, dict) and "array" in i:
+        return np.array(i["array"])
+    return i
+
+
+def index_arg(enc):
+    """The index of a getitem case (make_golden.enc_item encoding)."""
+    if "tuple" in enc:
+        return tuple(_dec_item(i) for i in enc["tuple"])
+    return _dec_item(enc["item"])

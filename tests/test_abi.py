@@ -50,6 +50,11 @@ def test_argument_errors(lib):
     assert b"empty reduction" in lib.bm_last_error()
     assert lib.bm_reduce(7, None, 10, 1, 1, 1, None, 10, None, 0, None) == -1
     assert lib.bm_reduce_combine(0, 10, None, None, 65, 1, None, 10, None) == -1
+    assert lib.bm_gather_rows(None, None, 1, 4, 0, None, 3, None) == -1
+    assert b"bad sizes" in lib.bm_last_error()
+    assert lib.bm_gather_rows(None, None, 1, 4, 8, None, 3, None) == -1
+    assert b"null pointer" in lib.bm_last_error()
+    assert lib.bm_gather_rows(None, None, 0, 4, 8, None, 3, None) == 0  # nothing to move
 
 
 def test_workspace_and_state_sizes(lib):

@@ -102,6 +102,25 @@ def _body(rank, world, device="cpu"):
     assert np.allclose(bt.mean(axis=0), t.mean(0)) and np.allclose(bt.std(), t.std())
     assert _exact(bolt.ones((3, 4), ctx, dtype=np.int32).toarray(), np.ones((3, 4), np.int32))
 
+    # indexing: every golden getitem / squeeze case (rows move between ranks
+    # for selections on the sharded axis; squeezing it re-slabs)
+    import golden_cases as G
+    for case in G.cases("getitem") + G.cases("squeeze"):
+        if "raises" in case or "collect_raises" in case:
+            continue
+        xg = G.make_input(case["input"])
+        bg = bolt.array(xg, ctx, axis=G.tup(case["axis"]))
+        if case["op"] == "squeeze":
+            r = bg.squeeze(G.tup(case["squeeze"]))
+            assert r.split == case["split"] and _exact(r.toarray(), G.arr(case, "out")), case["id"]
+            continue
+        r = bg[G.index_arg(case["index"])]
+        want = G.arr(case, "out_sorted" if case.get("toarray_unsorted") else "out")
+        if case["kind"] == "scalar":
+            assert np.asarray(r).tobytes() == want.tobytes(), case["id"]
+        else:
+            assert r.split == case["split"] and _exact(r.toarray(), want), case["id"]
+
 
 def _worker(rank, world, port, errq, device="cpu"):
     import torch.distributed as dist

@@ -153,3 +153,42 @@ def test_stat(case, bctx):
     else:
         truth = G.truth_stat(x, case["name"], ax)
         assert G.stat_close(got, want, truth, want.dtype, x)
+
+
+@pytest.mark.parametrize("case", G.cases("getitem"), ids=G.case_id)
+def test_getitem(case, bctx):
+    x, b = _b(case, bctx, case["npartitions"])
+    idx = G.index_arg(case["index"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            b[idx]
+        assert type(e.value).__name__ == case["raises"]
+        return
+    if "collect_raises" in case:
+        # the reference builds an array it cannot collect; this backend refuses the index
+        with pytest.raises(ValueError):
+            b[idx].toarray()
+        return
+    r = b[idx]
+    want = G.arr(case, "out_sorted" if case.get("toarray_unsorted") else "out")
+    if case["kind"] == "scalar":
+        assert type(r).__name__ == case["result_type"]
+        assert np.asarray(r).tobytes() == want.tobytes()
+        return
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    got = r.toarray()
+    assert got.dtype == want.dtype and got.tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("squeeze"), ids=G.case_id)
+def test_squeeze(case, bctx):
+    x, b = _b(case, bctx)
+    q = G.tup(case["squeeze"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            b.squeeze(q)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = b.squeeze(q)
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert r.toarray().tobytes() == G.arr(case, "out").tobytes()

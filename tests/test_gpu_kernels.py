@@ -112,6 +112,32 @@ def test_copy_strided_subbox_and_broadcast():
     assert np.all(_host(out3, np.float64, (1000,)) == 1.5)
 
 
+@pytest.mark.parametrize("shape,es", [((1, 5, 1), 8), ((3, 10, 7), 1), ((3, 10, 7), 2), ((4, 9, 33), 4),
+                                      ((2, 64, 1024), 16), ((1, 1 << 20, 1), 4), ((600, 37, 4), 4),
+                                      ((1, 1000, 3), 2), ((5, 17, 24), 8)])
+def test_gather_rows(shape, es):
+    """bm_gather_rows: x.take(idx, axis=1) on an (outer, rows, row) byte view,
+    unsorted and repeated indices, vector widths 1..16 B, unaligned offsets."""
+    import torch
+    be = _be()
+    n_outer, rows, row = shape
+    x = _rand((n_outer, rows, row * es), np.uint8, 7)
+    rng = np.random.default_rng(8)
+    for n_idx in (1, rows, 3 * rows + 1):
+        idx = rng.integers(0, rows, size=n_idx)
+        want = np.ascontiguousarray(x[:, idx, :])
+        for soff, doff in ((0, 0), (es, 0), (0, 2 * es), (1, 3)):
+            src = torch.zeros(x.nbytes + soff, dtype=torch.uint8, device="cuda")
+            src[soff:] = _dev(x)
+            out = torch.zeros(want.nbytes + doff + 64, dtype=torch.uint8, device="cuda")
+            be.gather_rows(src, soff, out, doff, n_outer, rows, row * es, idx)
+            got = out.cpu().numpy()
+            assert got[doff:doff + want.nbytes].tobytes() == want.tobytes(), (n_idx, soff, doff)
+            assert not got[:doff].any() and not got[doff + want.nbytes:].any()
+    with pytest.raises(IndexError):
+        be.gather_rows(src, 0, out, 0, n_outer, rows, row * es, [rows])
+
+
 def _ref_stats(x, O, R, I):
     v = x.reshape(O, R, I).astype(np.longdouble)
     mean = v.mean(axis=1)

@@ -148,3 +148,35 @@ def test_stats_full_size_c4_var(gpu_ctx):
     s = b.sum(axis=0)
     ref_s = (xs.sum(0).to(torch.int64) & 0xFFFF).cpu().numpy().astype(np.uint16)
     assert np.array_equal(np.asarray(s).reshape(-1)[cols.cpu().numpy()], ref_s)
+
+
+def test_getitem_full_size_c2(gpu_ctx):
+    """Indexing at the C2 size against torch index_select on the same bytes
+    (an independent device reference): reversed / strided slices, an int,
+    a list on the value and on the key axis, and a 1M-point advanced gather."""
+    import torch
+    shape = (2000, 512, 512)
+    b, raw = _shard(gpu_ctx, shape, np.float32, 1, 13)
+    x = raw.view(torch.float32).reshape(shape)
+
+    def sel(t, axis, idx):
+        return torch.index_select(t, axis, torch.as_tensor(np.asarray(idx), device="cuda"))
+
+    r = b[1999:0:-7, 100:400:3, ::-1]
+    want = sel(sel(sel(x, 0, np.arange(1999, 0, -7)), 1, np.arange(100, 400, 3)), 2, np.arange(511, -1, -1))
+    assert r.shape == tuple(want.shape) and torch.equal(r._data.view(torch.float32).reshape(want.shape), want)
+    r = b[:, 7]
+    assert r.shape == (2000, 512) and torch.equal(r._data.view(torch.float32).reshape(2000, 512), x[:, 7])
+    idx = [511, 0, 7, 300, 299]
+    r = b[:, :, idx]
+    assert torch.equal(r._data.view(torch.float32).reshape(2000, 512, 5), sel(x, 2, idx))
+    kidx = list(range(1999, -1, -3))
+    r = b[kidx]
+    assert torch.equal(r._data.view(torch.float32).reshape(len(kidx), 512, 512), sel(x, 0, kidx))
+    rng = np.random.default_rng(3)
+    pts = [np.sort(rng.integers(0, 2000, 1 << 20))] + [rng.integers(0, d, 1 << 20) for d in shape[1:]]
+    r = b[tuple(pts)]
+    lin = torch.as_tensor(np.ravel_multi_index(pts, shape), device="cuda")
+    # sorted keys: the reference's record order is the listed order only within a key's run
+    assert r.shape == (1 << 20,) and r.split == 1
+    assert torch.equal(r._data.view(torch.float32), x.reshape(-1)[lin])

@@ -143,3 +143,39 @@ def test_stat(case):
     else:
         truth = G.truth_stat(x, case["name"], ax)
         assert G.stat_close(got, want, truth, want.dtype, x)
+
+
+@pytest.mark.parametrize("case", G.cases("getitem"), ids=G.case_id)
+def test_getitem(case):
+    x, rs = _rs(case, case["npartitions"])
+    idx = G.index_arg(case["index"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.getitem(rs, idx)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = O.getitem(rs, idx)
+    if "collect_raises" in case:
+        with pytest.raises(ValueError):
+            O.toarray(r)
+        return
+    want = G.arr(case, "out_sorted" if case.get("toarray_unsorted") else "out")
+    if case["kind"] == "scalar":
+        assert type(r).__name__ == case["result_type"] and np.asarray(r).tobytes() == want.tobytes()
+        return
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert O.toarray(r).tobytes() == want.tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("squeeze"), ids=G.case_id)
+def test_squeeze(case):
+    x, rs = _rs(case)
+    q = G.tup(case["squeeze"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.squeeze(rs, q)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = O.squeeze(rs, q)
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert O.toarray(r).tobytes() == G.arr(case, "out").tobytes()

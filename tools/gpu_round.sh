@@ -7,4 +7,5 @@ if [ -n "$AB_LIBS" ]; then
 fi
 timeout -k 10 300 python tools/transfer_bench.py > gpurun_out/transfer.log 2>&1 || { echo TRANSFER_FAIL; exit 1; }
 timeout -k 10 300 python tools/chunk_bench.py > gpurun_out/chunk.log 2>&1 || { echo CHUNK_FAIL; exit 1; }
+timeout -k 10 300 python tools/index_bench.py > gpurun_out/index.log 2>&1 || { echo INDEX_FAIL; exit 1; }
 bash tools/gpu_bench_c2.sh
