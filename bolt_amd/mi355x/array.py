@@ -24,7 +24,7 @@ from bolt_amd.mi355x import _lib
 from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
 from bolt_amd.mi355x.context import contiguous_strides, local_shape
-from bolt_amd.mi355x.dist import all_gather_bytes, permute_sharded, redistribute_rows, select_sharded, _empty
+from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, permute_sharded, redistribute_rows, select_sharded, _empty
 from bolt_amd.mi355x.transfer import to_device, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
@@ -282,6 +282,118 @@ class BoltArrayMI355X(BoltArray):
         p[axis2] = axis1
         return self.transpose(p)
 
+    # ---------------------------------------------------------- functional
+    def stack(self, size=None):
+        """Group each partition's records into stacks of up to ``size`` (array.py:62-83)."""
+        from bolt_amd.mi355x.stack import StackedArrayMI355X
+        return StackedArrayMI355X._from_array(self, size)
+
+    def _align(self, axis):
+        """Swap so that ``axis`` are exactly the keys (array.py:85-115)."""
+        inshape(self.shape, axis)
+        tokeys = [(a - self._split) for a in axis if a >= self._split]
+        tovalues = [a for a in range(self._split) if a not in axis]
+        if tokeys or tovalues:
+            return self.swap(tovalues, tokeys)
+        return self
+
+    def first(self):
+        """The first record's value, on the host (array.py:117-123)."""
+        from bolt_amd.mi355x.dist import all_gather_bytes
+        rb = int(np.prod(self._shape[self._split:], dtype=np.int64)) * self._dtype.itemsize
+        buf = self._data[:rb]
+        if self._ctx.world_size > 1:
+            lo, hi = self._ctx.bounds(self._shape[0])[0]
+            sizes = [rb if r == 0 else 0 for r in range(self._ctx.world_size)]
+            buf = all_gather_bytes(self._ctx, buf if self._ctx.rank == 0 else buf[:0], sizes)
+        return BoltArrayLocal(to_host(buf, self._dtype, self._shape[self._split:]))
+
+    def _records_tensor(self):
+        """This rank's records as a (records, *value shape) torch view."""
+        from bolt_amd.mi355x import functional as F
+        lshape = self._local_shape
+        nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
+        return F.view(self._data, (nrec,) + tuple(self._shape[self._split:]), self._dtype)
+
+    def map(self, func, axis=(0,), value_shape=None, dtype=None, with_keys=False):
+        """Apply ``func`` to every record along ``axis`` (array.py:125-191).
+
+        The array is aligned (swapped) so ``axis`` are the keys, then ``func``
+        runs on every record -- a torch tensor on the GPU -- vmapped over all
+        of this rank's records at once (record by record with keys when
+        ``with_keys``: func((key tuple, value))).  Shape inference, checks and
+        the result's shape/split follow the reference.
+        """
+        from bolt_amd.mi355x import functional as F
+        axis = tupleize(axis)
+        swapped = self._align(axis)
+        dev = swapped._data.device
+        test_func = (lambda x: func(((0,), x))) if with_keys else func
+        if value_shape is None or dtype is None:
+            try:
+                mapped = F.to_device(test_func(F.random_like(swapped.values.shape, self._dtype, dev)), dev)
+            except Exception:
+                mapped = F.to_device(test_func(swapped._records_tensor()[0]), dev)
+            if value_shape is None:
+                value_shape = tuple(mapped.shape)
+            if dtype is None:
+                dtype = F.numpy_dtype(mapped.dtype)
+        value_shape = tupleize(value_shape)
+        dtype = np.dtype(dtype)
+        shape = tuple([swapped._shape[ax] for ax in range(len(axis))]) + value_shape
+        recs = swapped._records_tensor()
+        if with_keys:
+            import torch
+            lo, _ = swapped._ctx.local_bounds(swapped._shape[0]) if swapped._shape else (0, 0)
+            kshape = swapped._shape[:swapped._split]
+            base = lo * int(np.prod(kshape[1:], dtype=np.int64))
+            outs = [F.to_device(func((tuple(int(k) for k in np.unravel_index(base + i, kshape)), recs[i])), dev)
+                    for i in range(recs.shape[0])]
+            out = torch.stack(outs) if outs else None
+        else:
+            out = F.apply_batched(func, recs)
+        if out is not None and len(out.shape) > 1 and tuple(out.shape[1:]) != value_shape:
+            raise Exception("Map operation did not produce values of uniform shape.")
+        data = F.as_bytes(out.to(F.torch_dtype(dtype))) if out is not None else _empty(0, dev)
+        return self._like(data, shape, swapped.split, dtype=dtype)
+
+    def filter(self, func, axis=(0,), sort=False):
+        """Keep the records along ``axis`` for which ``func`` is true (array.py:193-241).
+
+        ``func`` runs on every record (a torch tensor, vmapped) and returns a
+        boolean; the kept records are compacted with one gather kernel (and an
+        all-to-all across GPUs) and re-keyed 0..count-1 in key order.
+        """
+        from bolt_amd.mi355x import functional as F
+        from bolt_amd.mi355x.indexing import gather_units_sharded
+        axis = tupleize(axis)
+        swapped = self._align(axis)
+        recs = swapped._records_tensor()
+        keep = F.apply_batched(lambda v: F.to_device(func(v), v.device).reshape(()).to(bool), recs)
+        mask = keep.cpu().numpy().reshape(-1) if keep is not None else np.zeros(0, bool)
+        ctx = swapped._ctx
+        local_idx = np.nonzero(mask)[0].astype(np.int64)
+        if ctx.world_size > 1:
+            import torch.distributed as dist
+            allm = [None] * ctx.world_size
+            dist.all_gather_object(allm, mask, group=ctx.group)
+            offs = np.r_[0, np.cumsum([m.size for m in allm])]
+            glob = np.concatenate([np.nonzero(m)[0] + offs[r] for r, m in enumerate(allm)]).astype(np.int64)
+        else:
+            glob = local_idx
+        remaining = list(swapped.shape[len(axis):])
+        count = int(glob.size)
+        es = self._dtype.itemsize
+        rowbytes = int(np.prod(remaining, dtype=np.int64)) * es
+        nrec = int(np.prod(swapped.shape[:swapped.split], dtype=np.int64))
+        if count == 0:
+            return self._like(_empty(0, swapped._data.device), (0,), 1)
+        # records are rows of the flattened key space; ragged per rank
+        flat_rows_per_lead = int(np.prod(swapped.shape[1:swapped.split], dtype=np.int64))
+        data = gather_units_sharded(ctx, swapped._backend, swapped._data, swapped.shape[0],
+                                    rowbytes, flat_rows_per_lead, glob, count, 1)
+        return self._like(data, tuple([count] + remaining), 1)
+
     # ------------------------------------------------------------ indexing
     def __getitem__(self, index):
         """Index with ints, slices and lists (array.py:595-676).
@@ -322,6 +434,52 @@ class BoltArrayMI355X(BoltArray):
         if len(int_locs) == self.ndim:
             return result.toarray().reshape(())[()]
         return result.squeeze(tuple(int_locs)) if int_locs else result
+
+    def concatenate(self, arry, axis=0):
+        """Join with another array along ``axis`` (array.py:429-478).
+
+        ndarrays (and local bolt arrays, which are ndarrays) are first built
+        as mi355x arrays keyed on this array's key axes, as the reference does;
+        the same shape checks and exceptions.  On the dense layout the result
+        is two strided copies (rows of the two inputs interleaved at the
+        concatenation axis); along the sharded leading axis across GPUs, one
+        all-to-all re-slabs the rows.
+        """
+        from bolt_amd.mi355x.construct import ConstructMI355X
+        if isinstance(arry, np.ndarray):
+            arry = ConstructMI355X.array(arry, self._ctx, axis=range(0, self._split))
+        elif not isinstance(arry, BoltArrayMI355X):
+            raise ValueError("other must be local array or mi355x array, got %s" % type(arry))
+        if not all([x == y if not i == axis else True
+                    for i, (x, y) in enumerate(zip(self.shape, arry.shape))]):
+            raise ValueError("all the input array dimensions except for "
+                             "the concatenation axis must match exactly")
+        if not self._split == arry.split:
+            raise NotImplementedError("two arrays must have the same split ")
+        if self.ndim != arry.ndim or not 0 <= axis < self.ndim:
+            raise ValueError("arrays of %d and %d dimensions cannot be joined on axis %d"
+                             % (self.ndim, arry.ndim, axis))
+        if arry.dtype != self._dtype:
+            raise NotImplementedError("concatenating %s with %s: cast one first (astype)"
+                                      % (self._dtype, arry.dtype))
+        shape = tuple([x + y if i == axis else x for i, (x, y) in enumerate(zip(self.shape, arry.shape))])
+        es = self._dtype.itemsize
+        if axis == 0:
+            rowbytes = int(np.prod(self._shape[1:], dtype=np.int64)) * es
+            data = concat_rows_sharded(self._ctx, self._data, self._shape[0], arry._data, arry.shape[0], rowbytes)
+            return self._like(data, shape, self._split)
+        lshape = self._local_shape
+        outer = int(np.prod(lshape[:axis], dtype=np.int64))
+        inner = int(np.prod(lshape[axis + 1:], dtype=np.int64))
+        na, nb = self._shape[axis] * inner, arry.shape[axis] * inner
+        data = _empty(outer * (na + nb) * es, self._data.device)
+        if outer:
+            be = self._backend
+            if na:
+                be.copy_strided(self._data, 0, data, 0, [outer, na], [na, 1], [na + nb, 1], es)
+            if nb:
+                be.copy_strided(arry._data, 0, data, na * es, [outer, nb], [nb, 1], [na + nb, 1], es)
+        return self._like(data, shape, self._split)
 
     def squeeze(self, axis=None):
         """Drop singleton axes (array.py:879-918); the data does not move on one

@@ -230,6 +230,131 @@ class ChunkedArrayMI355X(object):
         res._bare_singleton = bare
         return res
 
+    # ------------------------------------------------------------ functions
+    def _chunk_batches(self):
+        """(combo, batch) per run of equally shaped chunks: batch is a dense
+        (records x chunks-in-run, *padded chunk shape) tensor gathered from the
+        packed layout with one strided copy."""
+        from bolt_amd.mi355x import functional as F
+        es = self._dtype.itemsize
+        g = self._geom
+        n = len(g.vshape)
+        lshape = local_shape(self._ctx, self._shape)
+        nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
+        be = self._backend
+        for combo in g.copies(unpack=False):
+            shape, _, pstr, _, poff = combo
+            cnt, ex = shape[:n], shape[n:]
+            full = [nrec] + list(cnt) + list(ex)
+            nb = int(np.prod(full, dtype=np.int64)) * es
+            buf = _empty(nb, self._packed.device)
+            if nb:
+                dstr = [1] * len(full)
+                for k in range(len(full) - 2, -1, -1):
+                    dstr[k] = dstr[k + 1] * full[k + 1]
+                be.copy_strided(self._packed, poff * es, buf, 0, full, [g.size] + list(pstr), dstr, es)
+            yield combo, nrec, F.view(buf, [nrec * int(np.prod(cnt, dtype=np.int64))] + list(ex), self._dtype)
+
+    def _first_chunk(self):
+        from bolt_amd.mi355x import functional as F
+        cs = self._geom.chunk_shape(self._geom.chunk_ids()[0])
+        n = int(np.prod(cs, dtype=np.int64)) * self._dtype.itemsize
+        return F.view(self._packed[:n], cs, self._dtype)
+
+    def map(self, func, value_shape=None, dtype=None):
+        """Apply an array -> array function to every chunk (chunk.py:349-410).
+
+        ``func`` receives each chunk (with its padding) as a torch tensor on the
+        GPU; it is vmapped over all chunks of equal shape at once.  The same
+        shape inference, checks and exceptions as the reference: the function
+        may change only the unchunked axes; the result's plan is value_shape.
+        """
+        from bolt_amd.mi355x import functional as F
+        dev = self._packed.device
+        if value_shape is None or dtype is None:
+            try:
+                mapped = F.to_device(func(F.random_like(self.plan, self._dtype, dev)), dev)
+            except Exception:
+                mapped = F.to_device(func(self._first_chunk()), dev)
+            if value_shape is None:
+                value_shape = tuple(mapped.shape)
+            if dtype is None:
+                dtype = F.numpy_dtype(mapped.dtype)
+        dtype = np.dtype(dtype)
+        value_shape = tuple(int(v) for v in value_shape)
+        chunked = np.where(self.plan != self.vshape)[0]
+        unchunked = np.where(self.plan == self.vshape)[0]
+        if len(value_shape) != len(self.plan):
+            raise NotImplementedError('map on ChunkedArray cannot drop dimensions')
+        if any([value_shape[i] != self.plan[i] for i in chunked]):
+            raise ValueError('map cannot change the sizes of chunked dimensions')
+        vshape = [value_shape[i] if i in unchunked else int(self.vshape[i]) for i in range(len(self.vshape))]
+        newshape = tuple(int(k) for k in self.kshape) + tuple(vshape)
+        g2 = ChunkGeometry(vshape, value_shape, self._padding)
+        es2 = dtype.itemsize
+        lshape = local_shape(self._ctx, newshape)
+        nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
+        packed = _empty(nrec * g2.size * es2, dev)
+        n = len(vshape)
+        be = self._backend
+        tdt = F.torch_dtype(dtype)
+        for (combo, nrec_, batch), combo2 in zip(self._chunk_batches(), g2.copies(unpack=False)):
+            shape2, _, pstr2, _, poff2 = combo2
+            out = F.apply_batched(func, batch)
+            if out is None:
+                continue
+            new = tuple(out.shape[1:])
+            ex = tuple(batch.shape[1:])
+            if len(unchunked) and any(new[i] != value_shape[i] for i in unchunked):
+                raise Exception("Map operation did not produce values of uniform shape.")
+            if len(chunked) and any(ex[i] != new[i] for i in chunked):
+                raise Exception("Map operation changed the size of a chunked dimension")
+            if new != tuple(shape2[n:]):
+                raise Exception("Map operation did not produce values of uniform shape.")
+            src = F.as_bytes(out.to(tdt))
+            full = [nrec_] + list(shape2)
+            sstr = [1] * len(full)
+            for k in range(len(full) - 2, -1, -1):
+                sstr[k] = sstr[k + 1] * full[k + 1]
+            be.copy_strided(src, 0, packed, poff2 * es2, full, sstr, [g2.size] + list(pstr2), es2)
+        res = self._constructor(packed, shape=newshape, split=self._split, dtype=dtype, plan=value_shape,
+                                padding=self._padding, ordered=self._ordered, context=self._ctx)
+        res._bare_singleton = self._bare_singleton
+        return res
+
+    def map_generic(self, func):
+        """Apply an array -> object function to every chunk (chunk.py:412-432).
+
+        The reference returns an object-dtype BoltArraySpark of shape
+        kshape + number of chunks (split = its ndim); objects cannot live in
+        HBM, so the result here is that object array on the host, as a local
+        bolt array.  ``func`` receives each chunk as a torch tensor.
+        """
+        from bolt_amd.local import BoltArrayLocal
+        from bolt_amd.mi355x import functional as F
+        g = self._geom
+        es = self._dtype.itemsize
+        lshape = local_shape(self._ctx, self._shape)
+        nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
+        ids = g.chunk_ids()
+        objs = []
+        for r in range(nrec):
+            for j in ids:
+                cs = g.chunk_shape(j)
+                off = (r * g.size + g.chunk_offset(j)) * es
+                nb = int(np.prod(cs, dtype=np.int64)) * es
+                objs.append(func(F.view(self._packed[off:off + nb], cs, self._dtype)))
+        if self._ctx.world_size > 1:
+            import torch.distributed as dist
+            allobjs = [None] * self._ctx.world_size
+            dist.all_gather_object(allobjs, objs, group=self._ctx.group)
+            objs = [o for part in allobjs for o in part]
+        newshape = tuple(int(s) for s in np.r_[self.kshape, g.nchunks])
+        out = np.empty(len(objs), dtype=object)
+        for i, o in enumerate(objs):
+            out[i] = o
+        return BoltArrayLocal(out.reshape(newshape))
+
     # ------------------------------------------------------------- records
     def records(self):
         """((key..., chunk id...), chunk ndarray) in key order (``tordd().sortByKey()``)."""

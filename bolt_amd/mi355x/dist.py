@@ -287,6 +287,22 @@ def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es):
     return out
 
 
+def reslab_counts(ctx, data, counts, rowbytes):
+    """Rows held raggedly (rank r holds counts[r] consecutive rows, in rank
+    order) -> the standard slabs ctx.bounds(sum(counts)).  One all-to-all."""
+    if ctx.world_size == 1:
+        return data
+    starts = np.r_[0, np.cumsum(counts)].astype(np.int64)
+    ob = [(int(starts[q]) * rowbytes, int(starts[q + 1]) * rowbytes) for q in range(ctx.world_size)]
+    nb = [(lo * rowbytes, hi * rowbytes) for lo, hi in ctx.bounds(int(starts[-1]))]
+    r = ctx.rank
+    mlo, mhi = ob[r]
+    send_sizes = [max(0, min(mhi, qhi) - max(mlo, qlo)) for qlo, qhi in nb]
+    tlo, thi = nb[r]
+    recv_sizes = [max(0, min(thi, shi) - max(tlo, slo)) for slo, shi in ob]
+    return all_to_all_bytes(ctx, data, send_sizes, recv_sizes, _unit(rowbytes))
+
+
 def redistribute_rows(ctx, data, old_rows, old_rowbytes, new_rows, new_rowbytes):
     """Re-shard a flat byte array whose leading-axis extent changes (same bytes, new slabs).
 
@@ -303,3 +319,53 @@ def redistribute_rows(ctx, data, old_rows, old_rowbytes, new_rows, new_rowbytes)
     tlo, thi = nb[r]
     recv_sizes = [max(0, min(thi, shi) - max(tlo, slo)) for slo, shi in ob]
     return all_to_all_bytes(ctx, data, send_sizes, recv_sizes, _unit(np.gcd(old_rowbytes, new_rowbytes)))
+
+
+def concat_rows_sharded(ctx, a, a_rows, b, b_rows, rowbytes):
+    """This rank's slab of concatenate((A, B), axis=0) for row-sharded A and B.
+
+    The global byte sequence is A's then B's; every rank sends each peer the
+    parts of its two slabs that fall in the peer's output slab (one
+    all-to-all) and places what it receives by global offset.
+    """
+    out_rows = a_rows + b_rows
+    if ctx.world_size == 1:
+        out = _empty(out_rows * rowbytes, a.device)
+        out[:a.numel()].copy_(a)
+        out[a.numel():].copy_(b)
+        return out
+    r = ctx.rank
+    ab, bb, ob = ctx.bounds(a_rows), ctx.bounds(b_rows), ctx.bounds(out_rows)
+
+    def pieces(s, q):
+        """(global row lo, hi, source tensor, source row lo) sent from rank s to rank q."""
+        qlo, qhi = ob[q]
+        out = []
+        lo, hi = max(ab[s][0], qlo), min(ab[s][1], qhi)
+        if hi > lo:
+            out.append((lo, hi, "a", lo - ab[s][0]))
+        lo, hi = max(a_rows + bb[s][0], qlo), min(a_rows + bb[s][1], qhi)
+        if hi > lo:
+            out.append((lo, hi, "b", lo - a_rows - bb[s][0]))
+        return out
+
+    src = {"a": a, "b": b}
+    send_parts, send_sizes = [], []
+    for q in range(ctx.world_size):
+        ps = pieces(r, q)
+        send_sizes.append(sum(hi - lo for lo, hi, _, _ in ps) * rowbytes)
+        send_parts += [src[t][o * rowbytes:(o + hi - lo) * rowbytes] for lo, hi, t, o in ps]
+    import torch
+    send = torch.cat(send_parts) if send_parts else _empty(0, a.device)
+    recv_pieces = [pieces(s_, r) for s_ in range(ctx.world_size)]
+    recv_sizes = [sum(hi - lo for lo, hi, _, _ in ps) * rowbytes for ps in recv_pieces]
+    recv = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(rowbytes))
+    mlo = ob[r][0]
+    out = _empty((ob[r][1] - mlo) * rowbytes, a.device)
+    off = 0
+    for ps in recv_pieces:
+        for lo, hi, _, _ in ps:
+            n = (hi - lo) * rowbytes
+            out[(lo - mlo) * rowbytes:(lo - mlo) * rowbytes + n].copy_(recv[off:off + n])
+            off += n
+    return out

@@ -1,0 +1,95 @@
+"""User-function plumbing of the mi355x mode (map / map_generic / stack / filter).
+
+bolt applies numpy functions to records on Spark executors (chunk.py:349-432,
+stack.py:80-139, array.py:125-241).  Here records live in HBM, so the user
+function receives torch tensors on the array's device and should be written
+with torch operations (numpy-style spellings such as ``x.sum(axis=1,
+keepdims=True)`` work on tensors); a function that returns an ndarray has it
+moved to the device.  Record-wise functions are vectorised with torch.func.vmap
+over a batch of records or chunks (one launch per op for the whole batch); a
+function vmap cannot trace (data-dependent control flow, .item(), host
+numpy) is applied record by record, still on the device.
+"""
+import numpy as np
+
+_NP2TORCH = None
+
+
+def torch_dtype(dtype):
+    global _NP2TORCH
+    import torch
+    if _NP2TORCH is None:
+        _NP2TORCH = {np.dtype(k): v for k, v in [
+            (np.bool_, torch.bool), (np.uint8, torch.uint8), (np.int8, torch.int8),
+            (np.uint16, torch.uint16), (np.int16, torch.int16), (np.uint32, torch.uint32),
+            (np.int32, torch.int32), (np.uint64, torch.uint64), (np.int64, torch.int64),
+            (np.float16, torch.float16), (np.float32, torch.float32), (np.float64, torch.float64),
+            (np.complex64, torch.complex64), (np.complex128, torch.complex128)]}
+    try:
+        return _NP2TORCH[np.dtype(dtype)]
+    except KeyError:
+        raise NotImplementedError("dtype %s has no device representation" % np.dtype(dtype))
+
+
+def numpy_dtype(tdtype):
+    torch_dtype(np.float32)  # builds the table
+    for k, v in _NP2TORCH.items():
+        if v == tdtype:
+            return k
+    raise NotImplementedError("torch dtype %s has no numpy counterpart" % tdtype)
+
+
+def view(buf, shape, dtype):
+    """A uint8 buffer seen as a tensor of ``dtype`` and ``shape`` (no copy)."""
+    shape = tuple(int(s) for s in shape)
+    if buf.numel() == 0:
+        import torch
+        return torch.empty(shape, dtype=torch_dtype(dtype), device=buf.device)
+    return buf.view(torch_dtype(dtype)).reshape(shape)
+
+
+def as_bytes(t):
+    """A contiguous tensor's bytes as a flat uint8 tensor."""
+    import torch
+    t = t.contiguous()
+    if t.dtype == torch.bool:
+        t = t.view(torch.uint8)
+    return t.reshape(-1).view(torch.uint8) if t.numel() else torch.empty(0, dtype=torch.uint8, device=t.device)
+
+
+def to_device(out, device):
+    """A user function's result as a tensor on ``device`` (ndarrays / scalars are moved)."""
+    import torch
+    if isinstance(out, torch.Tensor):
+        return out if out.device == device else out.to(device)
+    return torch.as_tensor(np.asarray(out), device=device)
+
+
+def random_like(shape, dtype, device):
+    """randn(*shape).astype(dtype) on the device -- the probe the reference
+    feeds a function to learn its output shape (chunk.py:373-375, array.py:161)."""
+    import torch
+    r = torch.randn(tuple(int(s) for s in shape), dtype=torch.float64, device=device)
+    dt = np.dtype(dtype)
+    if dt.kind in "iub":
+        r = r.trunc()
+    return r.to(torch_dtype(dt))
+
+
+def apply_batched(func, batch):
+    """stack([func(batch[i]) for i]) -- vmapped when the function allows it."""
+    import torch
+    if batch.shape[0] == 0:
+        return None
+    try:
+        from torch.func import vmap
+        out = vmap(func)(batch)
+        if isinstance(out, torch.Tensor):
+            return out
+    except Exception:
+        pass
+    outs = [to_device(func(batch[i]), batch.device) for i in range(batch.shape[0])]
+    shapes = set(tuple(o.shape) for o in outs)
+    if len(shapes) != 1:
+        raise Exception("Map operation did not produce values of uniform shape.")
+    return torch.stack(outs)

@@ -226,6 +226,46 @@ def unchunk(cs):
     return RecSet([out], shape, split, cs.dtype)
 
 
+def chunk_map(cs, func, value_shape=None, dtype=None):
+    """ChunkedArray.map (chunk.py:349-410): func on every chunk; only unchunked
+    axes may change; the new plan is value_shape."""
+    if value_shape is None or dtype is None:
+        try:
+            mapped = func(np.random.randn(*cs.plan).astype(cs.dtype))
+        except Exception:
+            mapped = func(cs.records()[0][1])
+        value_shape = mapped.shape if value_shape is None else value_shape
+        dtype = mapped.dtype if dtype is None else dtype
+    chunked = np.where(cs.plan != cs.vshape)[0]
+    unchunked = np.where(cs.plan == cs.vshape)[0]
+    if len(value_shape) != len(cs.plan):
+        raise NotImplementedError('map on ChunkedArray cannot drop dimensions')
+    if any(value_shape[i] != cs.plan[i] for i in chunked):
+        raise ValueError('map cannot change the sizes of chunked dimensions')
+
+    def apply(v):
+        new = func(v)
+        if any(new.shape[i] != value_shape[i] for i in unchunked):
+            raise Exception("Map operation did not produce values of uniform shape.")
+        if any(v.shape[i] != new.shape[i] for i in chunked):
+            raise Exception("Map operation changed the size of a chunked dimension")
+        return new
+
+    parts = [[(k, apply(v)) for k, v in p] for p in cs.parts]
+    vshape = [value_shape[i] if i in unchunked else cs.vshape[i] for i in range(len(cs.vshape))]
+    shape = tuple(int(x) for x in np.r_[cs.kshape, vshape])
+    return ChunkSet(parts, shape, cs.split, dtype, value_shape, cs.padding)
+
+
+def chunk_map_generic(cs, func):
+    """ChunkedArray.map_generic (chunk.py:412-432): object per chunk, shape kshape + nchunks."""
+    recs = sorted(cs.records(), key=lambda kv: kv[0])
+    out = np.empty(len(recs), dtype=object)
+    for i, (_, v) in enumerate(recs):
+        out[i] = func(v)
+    return out.reshape(tuple(int(x) for x in np.r_[cs.kshape, _nchunks(cs.plan, cs.vshape)]))
+
+
 def keys_to_values(cs, axes, size=None):
     """ChunkedArray.keys_to_values (chunk.py:202-289): relabel, group by
     (stationary keys, new chunk ids, old chunk ids), stack each group."""
@@ -597,6 +637,135 @@ def getitem(rs, index):
     if len(int_locs) == nd:
         return toarray(squeeze(out)).reshape(())[()]
     return squeeze(out, tuple(int_locs))
+
+
+def concatenate(rs, other, axis=0):
+    """BoltArraySpark.concatenate (array.py:429-478): an ndarray is parallelized
+    on the same key axes; key axis -> union with shifted keys, value axis ->
+    join by key and numpy.concatenate of the two values."""
+    if isinstance(other, np.ndarray):
+        other = parallelize(other, axis=tuple(range(rs.split)))
+    elif not isinstance(other, RecSet):
+        raise ValueError("other must be local array or spark array, got %s" % type(other))
+    if not all(x == y or i == axis for i, (x, y) in enumerate(zip(rs.shape, other.shape))):
+        raise ValueError("all the input array dimensions except for the concatenation axis must match exactly")
+    if rs.split != other.split:
+        raise NotImplementedError("two arrays must have the same split ")
+    if axis < rs.split:
+        shift = rs.shape[axis]
+        moved = [(k[:axis] + (k[axis] + shift,) + k[axis + 1:], v) for k, v in other.records()]
+        parts = rs.parts + [moved]
+    else:
+        theirs = dict(other.records())
+        parts = [[(k, np.concatenate((v, theirs[k]), axis=axis - rs.split)) for k, v in p if k in theirs]
+                 for p in rs.parts]
+    shape = tuple(x + y if i == axis else x for i, (x, y) in enumerate(zip(rs.shape, other.shape)))
+    return RecSet(parts, shape, rs.split, rs.dtype)
+
+
+# ---------------------------------------------------------------- functional
+def align_keys(rs, axis):
+    """BoltArraySpark._align (array.py:85-115) for map/filter: swap so that axis are the keys."""
+    tokeys = [a - rs.split for a in axis if a >= rs.split]
+    tovalues = [a for a in range(rs.split) if a not in axis]
+    return swap(rs, tovalues, tokeys) if (tokeys or tovalues) else rs
+
+
+def map_(rs, func, axis=(0,), value_shape=None, dtype=None, with_keys=False):
+    """BoltArraySpark.map (array.py:125-191)."""
+    axis = tuple(axis)
+    sw = align_keys(rs, axis)
+    test = (lambda x: func(((0,), x))) if with_keys else func
+    if value_shape is None or dtype is None:
+        try:
+            mapped = test(np.random.randn(*sw.shape[sw.split:]).astype(rs.dtype))
+        except Exception:
+            mapped = test(sw.records()[0][1])
+        value_shape = mapped.shape if value_shape is None else value_shape
+        dtype = mapped.dtype if dtype is None else dtype
+    value_shape = tuple(value_shape)
+    parts = [[(k, func((k, v)) if with_keys else func(v)) for k, v in p] for p in sw.parts]
+    for p in parts:
+        for _, v in p:
+            if len(v.shape) > 0 and v.shape != value_shape:
+                raise Exception("Map operation did not produce values of uniform shape.")
+    shape = tuple(sw.shape[a] for a in range(len(axis))) + value_shape
+    return RecSet(parts, shape, sw.split, dtype)
+
+
+def filter_(rs, func, axis=(0,), sort=False):
+    """BoltArraySpark.filter (array.py:193-241): kept records renumbered in record order."""
+    axis = tuple(axis)
+    sw = align_keys(rs, axis)
+    kept = [(k, v) for k, v in sw.records() if func(v)]
+    if sort:
+        kept = sorted(kept, key=lambda kv: kv[0])
+    recs = [((i,), v) for i, (_, v) in enumerate(kept)]
+    shape = (len(recs),) + tuple(sw.shape[len(axis):]) if recs else (0,)
+    return RecSet([recs], shape, 1, sw.dtype)
+
+
+class StackSet(object):
+    """StackedArray (stack.py): per-partition stacks of (keys list, stacked values)."""
+
+    def __init__(self, parts, shape, split, rekeyed=False):
+        self.parts, self.shape, self.split, self.rekeyed = parts, tuple(shape), split, rekeyed
+
+    def records(self):
+        return [kv for p in self.parts for kv in p]
+
+
+def stack(rs, size=None):
+    """StackedArray.stack (stack.py:49-66)."""
+    parts = []
+    for p in rs.parts:
+        q, keys, vals = [], [], []
+        for k, v in p:
+            keys.append(k)
+            vals.append(v)
+            if size and 0 <= size <= len(keys):
+                q.append((keys, np.asarray(vals)))
+                keys, vals = [], []
+        if keys:
+            q.append((keys, np.asarray(vals)))
+        parts.append(q)
+    return StackSet(parts, rs.shape, rs.split)
+
+
+def stack_map(ss, func):
+    """StackedArray.map (stack.py:80-139)."""
+    vshape = ss.shape[ss.split:]
+    x = ss.records()[0][1]
+    a, b = (np.asarray([x]), np.asarray([x, x])) if x.shape == vshape else (x, np.concatenate((x, x)))
+    try:
+        at, bt = func(a), func(b)
+    except Exception as e:
+        raise RuntimeError("Error evaluating function on test array, got error:\n %s" % e)
+    if not (isinstance(at, np.ndarray) and isinstance(bt, np.ndarray)):
+        raise ValueError("Function must return ndarray")
+    if at.shape == bt.shape:
+        if ss.rekeyed:
+            parts = [[(k, func(v)) for k, v in p] for p in ss.parts]
+            shape = (ss.shape[0],) + at.shape
+        else:
+            vals = [func(v) for _, v in ss.records()]
+            parts = [[((i,), v) for i, v in enumerate(vals)]]
+            shape = (len(vals),) + at.shape
+        return StackSet(parts, shape, 1, True)
+    if at.shape[0] == a.shape[0] and bt.shape[0] == b.shape[0]:
+        parts = [[(k, func(v)) for k, v in p] for p in ss.parts]
+        return StackSet(parts, ss.shape[:ss.split] + at.shape[1:], ss.split, ss.rekeyed)
+    raise ValueError("Cannot infer effect of function on shape")
+
+
+def unstack(ss):
+    """StackedArray.unstack (stack.py:68-78)."""
+    if ss.rekeyed:
+        recs = ss.records()
+    else:
+        recs = [(k, v) for ks, vs in ss.records() for k, v in zip(ks, list(vs))]
+    dt = np.asarray(recs[0][1]).dtype if recs else np.float64
+    return RecSet([recs], ss.shape, ss.split, dt)
 
 
 def repartition(rs, n):

@@ -520,10 +520,174 @@ def gen_getitem():
             add(case, out=r.toarray())
 
 
+def gen_concatenate():
+    items = [((2, 3), (0,), (2, 3), (0,), 0), ((2, 3), (0,), (5, 3), (0,), 0), ((2, 3), (0,), (2, 4), (0,), 1),
+             ((4, 3, 5), (0, 1), (2, 3, 5), (0, 1), 0), ((4, 3, 5), (0, 1), (4, 6, 5), (0, 1), 1),
+             ((4, 3, 5), (0, 1), (4, 3, 2), (0, 1), 2), ((4, 3, 5), (0,), (4, 1, 5), (0,), 1),
+             ((4, 3, 5), (0,), (4, 3, 7), (0,), 2), ((3, 2, 2, 3), (0, 1, 2), (3, 2, 1, 3), (0, 1, 2), 2),
+             ((4, 3, 5), (0,), (4, 3, 6), (0,), 1), ((4, 3, 5), (0,), (4, 3, 5), (0, 1), 0),
+             ((7, 3), (0,), (9, 3), (0,), 0)]
+    for n, (sa, aa, sb, ab, axis) in enumerate(items):
+        specA = spec(sa, "float32", "normal", 30 + n)
+        specB = spec(sb, "float32", "normal", 60 + n)
+        x, y = make_input(specA), make_input(specB)
+        for kind in ("ndarray", "local", "spark"):
+            if kind != "spark" and ab != aa[:1] and ab != aa:
+                continue
+            for npart in (None, 3):
+                b = bolt.array(x, sc, axis=aa, npartitions=npart)
+                other = {"ndarray": lambda: y, "local": lambda: bolt.array(y),
+                         "spark": lambda: bolt.array(y, sc, axis=ab, npartitions=npart)}[kind]()
+                case = {"op": "concatenate", "input": specA, "axis": list(aa), "npartitions": npart,
+                        "other": specB, "other_axis": list(ab), "other_kind": kind, "cat_axis": axis}
+                r = run(lambda: b.concatenate(other, axis=axis), case)
+                if r is None:
+                    add(case)
+                    continue
+                case.update(shape=list(r.shape), split=r.split)
+                add(case, out=r.toarray())
+    x = make_input(spec((2, 3)))
+    case = {"op": "concatenate", "input": spec((2, 3)), "axis": [0], "npartitions": None, "other": None,
+            "other_axis": [0], "other_kind": "list", "cat_axis": 0}
+    run(lambda: bolt.array(x, sc).concatenate([[1, 2, 3]]), case)
+    add(case)
+
+
+def gen_chunk_map():
+    from funcs import FUNCS
+    items = [
+        (spec((4, 8, 8)), (0,), (4, 8), None, ["double", "crop_last", "dup_last", "flip_last", "shrink0",
+                                                 "first_row", "to_f64"]),
+        (spec((3, 10, 7), "float32", "normal", 40), (0,), (4, 7), (1, 0), ["affine", "square", "center0",
+                                                                          "dup_last", "to_f64"]),
+        (spec((2, 3, 6, 9, 5), "float64", "normal", 41), (0, 1), (3, 9, 5), (1, 0, 0), ["double", "norm_rows",
+                                                                                         "crop_last"]),
+        (spec((5, 12, 10), "float32", "normal", 42), (0,), (5, 4), (2, 1), ["affine", "flip_last"]),
+        (spec((4, 6), "int32", "ints", 43, small=1), (0,), (6,), None, ["double", "crop_last", "dup_last"]),
+    ]
+    for s, ax, size, pad, names in items:
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=ax)
+        c = b.chunk(size=size, padding=pad)
+        for name in names:
+            for vs in (None, "given"):
+                value_shape = None
+                if vs == "given":
+                    try:
+                        value_shape = FUNCS[name](np.zeros(tuple(c.plan), dtype=x.dtype)).shape
+                    except Exception:
+                        continue
+                case = {"op": "chunk_map", "input": s, "axis": list(ax), "npartitions": None,
+                        "size": list(size), "padding": list(pad) if pad else None, "func": name,
+                        "value_shape": list(value_shape) if value_shape is not None else None}
+                r = run(lambda: c.map(FUNCS[name], value_shape=value_shape), case)
+                if r is None:
+                    add(case)
+                    continue
+                u = run(lambda: r.unchunk().toarray(), case)
+                if u is None:
+                    case["unchunk_raises"] = case.pop("raises")
+                    add(case)
+                    continue
+                case.update(shape=list(r.shape), plan=[int(p) for p in r.plan], dtype=str(u.dtype))
+                add(case, out=u)
+    for s, size in [(spec((2, 8, 8)), (8, 5)), (spec((3, 4, 6)), (2, 3))]:
+        x = make_input(s)
+        c = bolt.array(x, sc).chunk(size=size)
+        d = c.map_generic(lambda v: [int(v.sum()), v.shape]).toarray()
+        flat = [list(o) for o in d.reshape(-1)]
+        add({"op": "chunk_map_generic", "input": s, "axis": [0], "npartitions": None, "size": list(size),
+             "shape": list(d.shape), "objects": [[o[0], list(o[1])] for o in flat]})
+
+
+def gen_functional():
+    from funcs import FUNCS
+    x10 = spec((10, 10))
+    x3 = spec((10, 10, 10), "float32", "normal", 50)
+    o2 = spec((100, 2), "float64", "normal", 51)
+    # stack / unstack
+    for s, ax, npart in [(x10, (0,), 2), (x10, (0,), 3), (x3, (0,), 2), (x3, (0, 1), 4), (o2, (0,), 2),
+                         (o2, (0,), 1)]:
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=ax, npartitions=npart)
+        for size in (None, 0, 2, 3, -1, 7):
+            st = b.stack(size)
+            recs = st._rdd.collect()
+            add({"op": "stack", "input": s, "axis": list(ax), "npartitions": npart, "size": size,
+                 "stack_shapes": [list(v.shape) for _, v in recs], "stack_keys": [[[int(q) for q in k] for k in ks]
+                                                                                for ks, _ in recs],
+                 "shape": list(st.shape), "split": st.split}, out=st.unstack().toarray())
+    # stacked map
+    chains = [["double"], ["sum1"], ["tile12"], ["ones22"], ["sum0"], ["arr1"], ["arr0"], ["double", "double"],
+              ["double", "ones22"], ["ones22", "double"], ["scalar2"], ["none"], ["zerodiv"], ["sum0", "double"],
+              ["square", "sum1"]]
+    for s, ax, npart, size in [(o2, (0,), 2, 5), (x3, (0,), 2, None), (x3, (0, 1), 3, 4), (x10, (0,), 1, 3)]:
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=ax, npartitions=npart)
+        for chain in chains:
+            case = {"op": "stack_map", "input": s, "axis": list(ax), "npartitions": npart, "size": size,
+                    "funcs": chain}
+
+            def go():
+                st = b.stack(size)
+                for name in chain:
+                    st = st.map(FUNCS[name])
+                return st.unstack()
+            r = run(go, case)
+            if r is None:
+                add(case)
+                continue
+            arr = r.toarray()
+            case.update(shape=list(r.shape), split=r.split, dtype=str(arr.dtype))
+            add(case, out=arr)
+    # BoltArraySpark.map / filter
+    y = spec((4, 5, 6), "float32", "normal", 52)
+    for s in (y, spec((4, 5, 6), "int64", "ints", 53, small=1)):
+        x = make_input(s)
+        for kax in ((0,), (0, 1)):
+            b = bolt.array(x, sc, axis=kax, npartitions=2)
+            for name, axis, vs, dt in [("double", (0,), None, None), ("sum0", (0,), None, None),
+                                       ("sum0", (0, 1), None, None), ("sum1", (2,), None, None),
+                                       ("double", (1, 2), None, None), ("to_f64", (0,), None, None),
+                                       ("double", (0,), "given", "given"), ("crop_last", (0, 2), None, None),
+                                       ("keyed", (0,), None, None), ("keyed", (1, 2), None, None)]:
+                with_keys = name == "keyed"
+                value_shape = dtype = None
+                if vs == "given":
+                    value_shape = tuple(x.shape[i] for i in range(x.ndim) if i not in axis)
+                    dtype = x.dtype
+                case = {"op": "map", "input": s, "axis": list(kax), "npartitions": 2, "func": name,
+                        "map_axis": list(axis), "value_shape": list(value_shape) if value_shape else None,
+                        "dtype": str(dtype) if dtype is not None else None, "with_keys": with_keys}
+                r = run(lambda: b.map(FUNCS[name], axis=axis, value_shape=value_shape, dtype=dtype,
+                                      with_keys=with_keys), case)
+                if r is None:
+                    add(case)
+                    continue
+                arr = r.toarray()
+                case.update(shape=list(r.shape), split=r.split, out_dtype=str(arr.dtype))
+                add(case, out=arr)
+            for name, axis, srt in [("gt_mean", (0,), False), ("gt_mean", (0, 1), True), ("gt_big", (2,), False),
+                                    ("never", (0,), False), ("gt_mean", (1, 2), False), ("gt_mean", (0, 1), False)]:
+                case = {"op": "filter", "input": s, "axis": list(kax), "npartitions": 2, "func": name,
+                        "filter_axis": list(axis), "sort": srt}
+                r = run(lambda: b.filter(FUNCS[name], axis=axis, sort=srt), case)
+                if r is None:
+                    add(case)
+                    continue
+                if r.shape == (0,):
+                    case.update(shape=[0], split=r.split)
+                    add(case)
+                    continue
+                case.update(shape=list(r.shape), split=r.split)
+                add(case, out=r.toarray())
+
+
 if __name__ == "__main__":
     sc = FakeContext(2)
     for g in (gen_construct, gen_swap, gen_transpose, gen_chunk, gen_moves, gen_getplan, gen_stats,
-              gen_stat_errors, gen_getitem):
+              gen_stat_errors, gen_getitem, gen_concatenate, gen_chunk_map,
+              gen_functional):
         try:
             g()
         except Exception:

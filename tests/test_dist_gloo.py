@@ -102,9 +102,49 @@ def _body(rank, world, device="cpu"):
     assert np.allclose(bt.mean(axis=0), t.mean(0)) and np.allclose(bt.std(), t.std())
     assert _exact(bolt.ones((3, 4), ctx, dtype=np.int32).toarray(), np.ones((3, 4), np.int32))
 
+    import golden_cases as G
+    # concatenation along the sharded axis re-slabs rows; along others it is local
+    for case in G.cases("concatenate"):
+        if "raises" in case:
+            continue
+        xg, yg = G.make_input(case["input"]), G.make_input(case["other"])
+        bg = bolt.array(xg, ctx, axis=G.tup(case["axis"]))
+        other = bolt.array(yg, ctx, axis=G.tup(case["other_axis"])) if case["other_kind"] == "spark" else yg
+        r = bg.concatenate(other, axis=case["cat_axis"])
+        assert _exact(r.toarray(), G.arr(case, "out")), case["id"]
+
+    # user functions: map / filter / chunk map everywhere; stacked maps whose
+    # result keeps the records (stacks are per-rank, so re-keyed counts differ)
+    from funcs import FUNCS
+    for case in G.cases("map") + G.cases("filter") + G.cases("chunk_map") + G.cases("stack_map"):
+        if "raises" in case:
+            continue
+        xg = G.make_input(case["input"])
+        bg = bolt.array(xg, ctx, axis=G.tup(case["axis"]))
+        if case["op"] == "map":
+            r = bg.map(FUNCS[case["func"]], axis=G.tup(case["map_axis"]), value_shape=G.tup(case["value_shape"]),
+                       dtype=case["dtype"], with_keys=case["with_keys"])
+        elif case["op"] == "filter":
+            r = bg.filter(FUNCS[case["func"]], axis=G.tup(case["filter_axis"]), sort=case["sort"])
+            if case["shape"] == [0]:
+                assert r.shape == (0,)
+                continue
+        elif case["op"] == "chunk_map":
+            c = bg.chunk(size=G.size_arg(case["size"]), padding=G.tup(case["padding"]))
+            r = c.map(FUNCS[case["func"]], value_shape=G.tup(case["value_shape"])).unchunk()
+        else:
+            if case["shape"][:1] != case["input"]["shape"][:1]:
+                continue
+            st = bg.stack(case["size"])
+            for name in case["funcs"]:
+                st = st.map(FUNCS[name])
+            r = st.unstack()
+        got, want = r.toarray(), G.arr(case, "out")
+        assert got.shape == want.shape and got.dtype == want.dtype, case["id"]
+        assert np.allclose(got, want, rtol=1e-5, atol=1e-5 * float(np.max(np.abs(want)))), case["id"]
+
     # indexing: every golden getitem / squeeze case (rows move between ranks
     # for selections on the sharded axis; squeezing it re-slabs)
-    import golden_cases as G
     for case in G.cases("getitem") + G.cases("squeeze"):
         if "raises" in case or "collect_raises" in case:
             continue

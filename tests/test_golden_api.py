@@ -192,3 +192,112 @@ def test_squeeze(case, bctx):
     r = b.squeeze(q)
     assert list(r.shape) == case["shape"] and r.split == case["split"]
     assert r.toarray().tobytes() == G.arr(case, "out").tobytes()
+
+
+def _other(case, bctx):
+    y = G.make_input(case["other"]) if case["other"] else [[1, 2, 3]]
+    kind = case["other_kind"]
+    if kind == "local":
+        return bolt.array(y)
+    if kind == "spark":
+        return bolt.array(y, bctx, axis=G.tup(case["other_axis"]), npartitions=case["npartitions"])
+    return y
+
+
+@pytest.mark.parametrize("case", G.cases("concatenate"), ids=G.case_id)
+def test_concatenate(case, bctx):
+    x, b = _b(case, bctx, case["npartitions"])
+    other = _other(case, bctx)
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            b.concatenate(other, axis=case["cat_axis"])
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = b.concatenate(other, axis=case["cat_axis"])
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert r.toarray().tobytes() == G.arr(case, "out").tobytes()
+
+
+def _close(got, want, exact):
+    if exact:
+        return got.dtype == want.dtype and got.tobytes() == want.tobytes()
+    rtol = 1e-6 if want.dtype == np.float32 else 1e-12
+    scale = float(np.max(np.abs(want))) if want.size else 0.0
+    return got.dtype == want.dtype and np.allclose(got, want, rtol=rtol, atol=rtol * scale)
+
+
+@pytest.mark.parametrize("case", G.cases("chunk_map"), ids=G.case_id)
+def test_chunk_map(case, bctx):
+    from funcs import FUNCS, EXACT
+    x, b = _b(case, bctx)
+    c = b.chunk(size=G.size_arg(case["size"]), padding=G.tup(case["padding"]))
+    f = FUNCS[case["func"]]
+    vs = G.tup(case["value_shape"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            c.map(f, value_shape=vs)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = c.map(f, value_shape=vs)
+    assert list(r.shape) == case["shape"] and list(r.plan) == case["plan"]
+    assert _close(r.unchunk().toarray(), G.arr(case, "out"), case["func"] in EXACT)
+
+
+@pytest.mark.parametrize("case", G.cases("chunk_map_generic"), ids=G.case_id)
+def test_chunk_map_generic(case, bctx):
+    x, b = _b(case, bctx)
+    c = b.chunk(size=G.size_arg(case["size"]))
+    d = c.map_generic(lambda v: [int(v.sum()), list(v.shape)])
+    assert list(d.shape) == case["shape"]
+    assert [list(o) for o in np.asarray(d).reshape(-1)] == case["objects"]
+
+
+@pytest.mark.parametrize("case", G.cases("stack"), ids=G.case_id)
+def test_stack(case, bctx):
+    x, b = _b(case, bctx, case["npartitions"])
+    st = b.stack(case["size"])
+    recs = st.tordd().collect()
+    assert [list(v.shape) for _, v in recs] == case["stack_shapes"]
+    assert [[list(k) for k in ks] for ks, _ in recs] == case["stack_keys"]
+    assert list(st.shape) == case["shape"] and st.split == case["split"]
+    assert st.unstack().toarray().tobytes() == G.arr(case, "out").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("stack_map"), ids=G.case_id)
+def test_stack_map(case, bctx):
+    from funcs import FUNCS, EXACT
+    x, b = _b(case, bctx, case["npartitions"])
+
+    def go():
+        st = b.stack(case["size"])
+        for name in case["funcs"]:
+            st = st.map(FUNCS[name])
+        return st.unstack()
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            go()
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = go()
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert _close(r.toarray(), G.arr(case, "out"), all(f in EXACT for f in case["funcs"]))
+
+
+@pytest.mark.parametrize("case", G.cases("map"), ids=G.case_id)
+def test_map(case, bctx):
+    from funcs import FUNCS, EXACT
+    x, b = _b(case, bctx, case["npartitions"])
+    r = b.map(FUNCS[case["func"]], axis=G.tup(case["map_axis"]), value_shape=G.tup(case["value_shape"]),
+              dtype=case["dtype"], with_keys=case["with_keys"])
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert _close(r.toarray(), G.arr(case, "out"), case["func"] in EXACT)
+
+
+@pytest.mark.parametrize("case", G.cases("filter"), ids=G.case_id)
+def test_filter(case, bctx):
+    from funcs import FUNCS
+    x, b = _b(case, bctx, case["npartitions"])
+    r = b.filter(FUNCS[case["func"]], axis=G.tup(case["filter_axis"]), sort=case["sort"])
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    if case["shape"] != [0]:
+        assert r.toarray().tobytes() == G.arr(case, "out").tobytes()

@@ -179,3 +179,105 @@ def test_squeeze(case):
     r = O.squeeze(rs, q)
     assert list(r.shape) == case["shape"] and r.split == case["split"]
     assert O.toarray(r).tobytes() == G.arr(case, "out").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("concatenate"), ids=G.case_id)
+def test_concatenate(case):
+    x, rs = _rs(case, case["npartitions"])
+    if case["other"] is None:
+        other = [[1, 2, 3]]
+    else:
+        y = G.make_input(case["other"])
+        other = y if case["other_kind"] != "spark" else O.parallelize(y, axis=G.tup(case["other_axis"]))
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.concatenate(rs, other, case["cat_axis"])
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = O.concatenate(rs, other, case["cat_axis"])
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert O.toarray(r).tobytes() == G.arr(case, "out").tobytes()
+
+
+def _close(got, want, exact):
+    if exact:
+        return got.dtype == want.dtype and got.tobytes() == want.tobytes()
+    rtol = 1e-6 if want.dtype == np.float32 else 1e-12
+    scale = float(np.max(np.abs(want))) if want.size else 0.0
+    return got.dtype == want.dtype and np.allclose(got, want, rtol=rtol, atol=rtol * scale)
+
+
+@pytest.mark.parametrize("case", G.cases("chunk_map"), ids=G.case_id)
+def test_chunk_map(case):
+    from funcs import FUNCS, EXACT
+    x, rs = _rs(case)
+    c = O.chunk(rs, G.size_arg(case["size"]), None, G.tup(case["padding"]))
+    f = FUNCS[case["func"]]
+    vs = G.tup(case["value_shape"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            O.chunk_map(c, f, vs)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = O.chunk_map(c, f, vs)
+    assert list(r.shape) == case["shape"] and list(r.plan) == case["plan"]
+    assert _close(O.toarray(O.unchunk(r)), G.arr(case, "out"), case["func"] in EXACT)
+
+
+@pytest.mark.parametrize("case", G.cases("chunk_map_generic"), ids=G.case_id)
+def test_chunk_map_generic(case):
+    x, rs = _rs(case)
+    c = O.chunk(rs, G.size_arg(case["size"]))
+    d = O.chunk_map_generic(c, lambda v: [int(v.sum()), list(v.shape)])
+    assert list(d.shape) == case["shape"]
+    assert [list(o) for o in d.reshape(-1)] == case["objects"]
+
+
+@pytest.mark.parametrize("case", G.cases("stack"), ids=G.case_id)
+def test_stack(case):
+    x, rs = _rs(case, case["npartitions"])
+    st = O.stack(rs, case["size"])
+    recs = st.records()
+    assert [list(v.shape) for _, v in recs] == case["stack_shapes"]
+    assert [[list(k) for k in ks] for ks, _ in recs] == case["stack_keys"]
+    assert O.toarray(O.unstack(st)).tobytes() == G.arr(case, "out").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("stack_map"), ids=G.case_id)
+def test_stack_map(case):
+    from funcs import FUNCS, EXACT
+    x, rs = _rs(case, case["npartitions"])
+
+    def go():
+        st = O.stack(rs, case["size"])
+        for name in case["funcs"]:
+            st = O.stack_map(st, FUNCS[name])
+        return O.unstack(st)
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            go()
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = go()
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert _close(O.toarray(r), G.arr(case, "out"), all(f in EXACT for f in case["funcs"]))
+
+
+@pytest.mark.parametrize("case", G.cases("map"), ids=G.case_id)
+def test_map(case):
+    from funcs import FUNCS, EXACT
+    x, rs = _rs(case, case["npartitions"])
+    r = O.map_(rs, FUNCS[case["func"]], G.tup(case["map_axis"]), G.tup(case["value_shape"]), case["dtype"],
+               case["with_keys"])
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert _close(O.toarray(r), G.arr(case, "out"), case["func"] in EXACT)
+
+
+@pytest.mark.parametrize("case", G.cases("filter"), ids=G.case_id)
+def test_filter(case):
+    from funcs import FUNCS
+    x, rs = _rs(case, case["npartitions"])
+    r = O.filter_(rs, FUNCS[case["func"]], G.tup(case["filter_axis"]), case["sort"])
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    if case["shape"] != [0]:
+        assert O.toarray(r).tobytes() == G.arr(case, "out").tobytes()
