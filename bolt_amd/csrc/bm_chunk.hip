@@ -1,0 +1,174 @@
+// bm_chunk.hip -- record-map gather of libbolt_mi355x (gfx950): chunk pack /
+// unpack of small records.
+//
+// ChunkedArray._chunk (bolt/spark/chunk.py:87-144) cuts every record's value
+// block into the same set of (padded) chunks, and unchunk/removepad
+// (chunk.py:146-200, :514-550) stitches them back; the layout change is the
+// same for every record.  The host turns it into one int32 map per
+// direction (plan.ChunkGeometry.record_map):
+//
+//     dst[r * dst_rec + o] = src[r * src_rec + map[o]]      o < dst_rec
+//
+// When a source record fits in LDS (C5: 64x64 float64 = 32 KiB; padded
+// 16x16 chunks with 2-cell halos are 160-B rows that a strided copy reads
+// badly), a block stages whole records with 16-B loads (records are
+// contiguous, so a tile of RB records is one contiguous read), then writes
+// the destination records contiguously, VEC elements per lane, picking each
+// element out of LDS through the map (int32, L2-resident, shared by all
+// records).  HBM traffic = the algorithmic bytes: src_rec + dst_rec element
+// bytes per record, each byte moved once; the halo re-reads come from LDS.
+// Larger records use the direct form (map lookups straight from HBM/L2).
+#include "bm_common.h"
+#include "../../include/bolt_mi355x.h"
+
+namespace {
+
+constexpr int kCThreads = 256;
+constexpr int64_t kStageBytes = 32768;   // LDS per tile when records are small (5 blocks / CU)
+constexpr int64_t kMaxStageBytes = 65536;
+
+template <int ES> struct Elem;
+template <> struct Elem<1> { typedef uint8_t t; };
+template <> struct Elem<2> { typedef uint16_t t; };
+template <> struct Elem<4> { typedef uint32_t t; };
+template <> struct Elem<8> { typedef uint64_t t; };
+
+// LB: staging load width in bytes (16 when the tile's bytes are 16-B aligned)
+template <int ES, int VEC, int LB>
+__global__ void __launch_bounds__(kCThreads)
+    k_recmap_lds(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ map,
+                 int64_t src_rec, int64_t dst_rec, int64_t nrec, int64_t rb, FastDiv fdst) {
+  typedef typename Elem<ES>::t T;
+  typedef typename VecB<LB>::t L;
+  typedef typename VecB<ES * VEC>::t V;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const T *lds = reinterpret_cast<const T *>(smem);
+  const int64_t ntiles = (nrec + rb - 1) / rb;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t r0 = t * rb;
+    const int64_t nr = min(rb, nrec - r0);
+    // stage nr contiguous source records
+    const int64_t nld = nr * src_rec * ES / LB;
+    const L *s = reinterpret_cast<const L *>(src + r0 * src_rec * ES);
+    L *sl = reinterpret_cast<L *>(smem);
+    for (int64_t i = threadIdx.x; i < nld; i += kCThreads) sl[i] = __builtin_nontemporal_load(s + i);
+    __syncthreads();
+    // gather nr destination records, VEC elements per lane
+    const int64_t nout = nr * dst_rec / VEC;
+    V *d = reinterpret_cast<V *>(dst + r0 * dst_rec * ES);
+    for (int64_t i = threadIdx.x; i < nout; i += kCThreads) {
+      const uint64_t e = (uint64_t)i * VEC;
+      const uint64_t r = fd_div(e, fdst);
+      const int64_t o = (int64_t)(e - r * fdst.d);
+      const T *rl = lds + r * src_rec;
+      T v[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) v[k] = rl[map[o + k]];
+      V w;
+      __builtin_memcpy(&w, v, sizeof(V));
+      __builtin_nontemporal_store(w, d + i);
+    }
+    __syncthreads();
+  }
+}
+
+template <int ES>
+__global__ void __launch_bounds__(kCThreads)
+    k_recmap_direct(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ map,
+                    int64_t src_rec, uint64_t total, FastDiv fdst) {
+  typedef typename Elem<ES>::t T;
+  const T *s = reinterpret_cast<const T *>(src);
+  T *d = reinterpret_cast<T *>(dst);
+  const uint64_t step = (uint64_t)gridDim.x * kCThreads;
+  for (uint64_t g = (uint64_t)blockIdx.x * kCThreads + threadIdx.x; g < total; g += step) {
+    const uint64_t r = fd_div(g, fdst);
+    const int64_t o = (int64_t)(g - r * fdst.d);
+    d[g] = s[(int64_t)r * src_rec + map[o]];
+  }
+}
+
+template <int ES, int VEC>
+void launch_lds_v(const char *src, char *dst, const int32_t *map, int64_t src_rec, int64_t dst_rec,
+                  int64_t nrec, int64_t rb, int lb, int grid, size_t shmem, hipStream_t st) {
+  const FastDiv f = make_fastdiv((uint64_t)dst_rec);
+  switch (lb) {
+    case 16: k_recmap_lds<ES, VEC, 16><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
+    case 8: k_recmap_lds<ES, VEC, 8><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
+    case 4: k_recmap_lds<ES, VEC, 4><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
+    case 2: k_recmap_lds<ES, VEC, 2><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
+    default: k_recmap_lds<ES, VEC, 1><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
+  }
+}
+
+template <int ES>
+void launch_lds(const char *src, char *dst, const int32_t *map, int64_t src_rec, int64_t dst_rec,
+                int64_t nrec, int64_t rb, int lb, int vec, int grid, size_t shmem, hipStream_t st) {
+  constexpr int V16 = 16 / ES;
+  if (vec >= V16) return launch_lds_v<ES, V16>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
+  if (ES <= 4 && vec >= 8 / ES)
+    return launch_lds_v<ES, (8 / ES > 0 ? 8 / ES : 1)>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
+  if (ES <= 2 && vec >= 4 / ES)
+    return launch_lds_v<ES, (4 / ES > 0 ? 4 / ES : 1)>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
+  if (ES == 1 && vec >= 2) return launch_lds_v<ES, 2>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
+  launch_lds_v<ES, 1>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
+}
+
+int pow2_align(uintptr_t a, int64_t bytes, int cap) {
+  int w = cap;
+  while (w > 1 && (((a % (uintptr_t)w) != 0) || (bytes % w) != 0)) w >>= 1;
+  return w;
+}
+
+}  // namespace
+
+extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int64_t src_rec, int64_t dst_rec,
+                                const int32_t *map, int elem_bytes, void *stream) {
+  if (nrec < 0 || src_rec <= 0 || dst_rec <= 0 || src_rec > 0x7fffffffLL ||
+      (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8)) {
+    bm_set_error("bm_record_gather: bad arguments (nrec %lld, src_rec %lld, dst_rec %lld, elem_bytes %d)",
+                 (long long)nrec, (long long)src_rec, (long long)dst_rec, elem_bytes);
+    return BM_E_ARG;
+  }
+  if (nrec == 0) return BM_OK;
+  if (!src_ || !dst_ || !map) {
+    bm_set_error("bm_record_gather: null pointer");
+    return BM_E_ARG;
+  }
+  const char *src = static_cast<const char *>(src_);
+  char *dst = static_cast<char *>(dst_);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int es = elem_bytes;
+  const int64_t rec_bytes = src_rec * es;
+  if (rec_bytes <= kMaxStageBytes) {
+    int64_t rb = rec_bytes >= kStageBytes ? 1 : kStageBytes / rec_bytes;
+    if (rb > nrec) rb = nrec;
+    const int64_t ntiles = (nrec + rb - 1) / rb;
+    const size_t shmem = (size_t)(rb * rec_bytes + 15) / 16 * 16;
+    const int lb = pow2_align((uintptr_t)src, rec_bytes, 16);          // every tile start aligned
+    const int vec = pow2_align((uintptr_t)dst, dst_rec * es, 16) / es;  // elements per store
+    const int grid = (int)(ntiles < 16384 ? ntiles : 16384);
+    switch (es) {
+      case 1: launch_lds<1>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
+      case 2: launch_lds<2>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
+      case 4: launch_lds<4>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
+      default: launch_lds<8>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
+    }
+  } else {
+    const uint64_t total = (uint64_t)nrec * (uint64_t)dst_rec;
+    uint64_t g = (total + kCThreads - 1) / kCThreads;
+    if (g > 1048576) g = 1048576;
+    const FastDiv f = make_fastdiv((uint64_t)dst_rec);
+    switch (es) {
+      case 1: k_recmap_direct<1><<<(int)g, kCThreads, 0, st>>>(src, dst, map, src_rec, total, f); break;
+      case 2: k_recmap_direct<2><<<(int)g, kCThreads, 0, st>>>(src, dst, map, src_rec, total, f); break;
+      case 4: k_recmap_direct<4><<<(int)g, kCThreads, 0, st>>>(src, dst, map, src_rec, total, f); break;
+      default: k_recmap_direct<8><<<(int)g, kCThreads, 0, st>>>(src, dst, map, src_rec, total, f); break;
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    bm_set_error("bm_record_gather: launch failed: %s", hipGetErrorString(e));
+    return BM_E_HIP;
+  }
+  return BM_OK;
+}

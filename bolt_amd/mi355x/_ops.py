@@ -49,6 +49,7 @@ class HipBackend(object):
 
     def __init__(self):
         self.lib = _lib.load()
+        self._maps = {}  # (device, geometry key) -> resident int32 record map
 
     @staticmethod
     def _stream(t):
@@ -88,6 +89,25 @@ class HipBackend(object):
                                            int(idx.size), self._stream(src)), "bm_gather_rows")
         # the caching allocator must not hand the index buffer out before the kernel has read it
         didx.record_stream(torch.cuda.current_stream(src.device))
+
+    def record_gather(self, src, src_off, dst, dst_off, nrec, src_rec, dst_rec, rmap, key, es):
+        """dst[r*dst_rec + o] = src[r*src_rec + rmap[o]] (elements; offsets in bytes).
+
+        rmap: host int32 array of dst_rec entries in [0, src_rec), uploaded once
+        per (device, key) and kept resident.
+        """
+        import torch
+        ck = (src.device, key)
+        dmap = self._maps.get(ck)
+        if dmap is None:
+            rmap = np.ascontiguousarray(rmap, dtype=np.int32)
+            if rmap.size != dst_rec or rmap.min() < 0 or rmap.max() >= src_rec:
+                raise ValueError("record map does not match the record sizes")
+            dmap = torch.from_numpy(rmap).to(src.device)
+            self._maps[ck] = dmap
+        _lib.check(self.lib.bm_record_gather(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
+                                             int(src_rec), int(dst_rec), ctypes.c_void_p(dmap.data_ptr()),
+                                             int(es), self._stream(src)), "bm_record_gather")
 
     def _workspace(self, stat, code, O, R, I, device):
         import torch

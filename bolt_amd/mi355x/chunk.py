@@ -12,12 +12,29 @@ moved axes; their result is by construction the chunking of the permuted
 array with the new plan/padding (chunk.py:202-347), so they run as
 unpack -> permute (RCCL all-to-all if the sharded axis moves) -> pack.
 """
+import os
+
 import numpy as np
 
 from bolt_amd.mi355x.context import local_shape
 from bolt_amd.mi355x.dist import permute_sharded, _empty
 from bolt_amd.mi355x.plan import (ChunkGeometry, getplan, check_plan, getnumber, getslices, getmask,
-                           removepad_slices)
+                                  removepad_slices, k2v_copies, v2k_copies, copies_to_map)
+
+
+RECORD_MAP_MAX_BYTES = 65536  # a source record staged whole in LDS (bm_record_gather)
+
+
+def _fused_rechunk():
+    """keys_to_values / values_to_keys packed -> packed (A/B knob BOLT_AMD_FUSED_RECHUNK=0)."""
+    return os.environ.get("BOLT_AMD_FUSED_RECHUNK", "1") != "0"
+
+
+def _use_record_map(src_rec, es):
+    """Small records: one record-map gather instead of a strided copy per chunk run."""
+    if os.environ.get("BOLT_AMD_RECORD_MAP", "1") == "0":  # A/B knob
+        return False
+    return es in (1, 2, 4, 8) and 0 < src_rec * es <= RECORD_MAP_MAX_BYTES
 
 
 class ChunkedArrayMI355X(object):
@@ -119,7 +136,10 @@ class ChunkedArrayMI355X(object):
         geom = ChunkGeometry(vshape, plan, padding)
         rec = int(np.prod(vshape, dtype=np.int64))
         packed = _empty(nrec * geom.size * es, dense.device)
-        if nrec:
+        if nrec and _use_record_map(rec, es):
+            backend.record_gather(dense, 0, packed, 0, nrec, rec, geom.size,
+                                  geom.record_map(unpack=False), ("pack",) + geom.key(), es)
+        elif nrec:
             for (cshape, dstr, pstr, doff, poff) in geom.copies(unpack=False):
                 backend.copy_strided(dense, doff * es, packed, poff * es, [nrec] + cshape,
                                      [rec] + dstr, [geom.size] + pstr, es)
@@ -170,6 +190,23 @@ class ChunkedArrayMI355X(object):
         return self._constructor(packed, shape=newshape, split=newsplit, dtype=self._dtype,
                                  plan=newplan, padding=newpadding, ordered=True, context=self._ctx)
 
+    def _repack(self, copies, rmap, newshape, newsplit, newplan, newpadding, new):
+        """New packing straight from this packing: strided copies or one record-map gather."""
+        es = self._dtype.itemsize
+        lnew = local_shape(self._ctx, newshape)
+        nrec = int(np.prod(lnew[:newsplit], dtype=np.int64))
+        packed = _empty(nrec * new.size * es, self._packed.device)
+        be = self._backend
+        if nrec and rmap is not None:
+            nold = int(np.prod(local_shape(self._ctx, self._shape)[:self._split], dtype=np.int64))
+            m, key = rmap
+            be.record_gather(self._packed, 0, packed, 0, nold, self._geom.size, m.size, m, key, es)
+        elif nrec:
+            for shape, ss, ds, so, do in copies:
+                be.copy_strided(self._packed, so * es, packed, do * es, shape, ss, ds, es)
+        return self._constructor(packed, shape=newshape, split=newsplit, dtype=self._dtype,
+                                 plan=newplan, padding=newpadding, ordered=True, context=self._ctx)
+
     # ------------------------------------------------------------- the API
     def unchunk(self):
         """Back to a BoltArrayMI355X (chunk.py:146-200); a trailing (1,) value axis is squeezed."""
@@ -195,8 +232,15 @@ class ChunkedArrayMI355X(object):
         newpadding = np.r_[np.zeros(len(axes), dtype=int), self.padding].astype(int)
         ks = np.arange(self._split)
         perm = list(ks[~kmask]) + list(ks[kmask]) + list(range(self._split, len(self._shape)))
+        squeeze = np.array_equal(self.vshape, [1])
+        if _fused_rechunk() and not squeeze and (self._ctx.world_size == 1 or not kmask[0]):
+            # packed -> packed in one pass: no exchange, no dense intermediate
+            new = ChunkGeometry(newshape[newsplit:], newplan, newpadding)
+            lk = [int(k) for k in local_shape(self._ctx, self._shape)[:self._split]]
+            copies = k2v_copies(self._geom, new, lk, kmask)
+            return self._repack(copies, None, newshape, newsplit, newplan, newpadding, new)
         dense = self._unpack()
-        if np.array_equal(self.vshape, [1]):
+        if squeeze:
             # the singleton value axis of an all-keys chunking is squeezed
             # (chunk.py:284-287; padding and stale chunk id trimmed as numpy<1.13 did)
             newshape = newshape[:-1]
@@ -216,6 +260,20 @@ class ChunkedArrayMI355X(object):
         vs = np.arange(len(self.vshape))
         perm = (list(range(self._split)) + [self._split + v for v in vs[vmask]] +
                 [self._split + v for v in vs[~vmask]])
+        if _fused_rechunk() and len(newshape) > newsplit:
+            # the leading key never moves: always local, packed -> packed in one pass
+            new = ChunkGeometry(newshape[newsplit:], newplan, newpadding)
+            lk = [int(k) for k in local_shape(self._ctx, self._shape)[:self._split]]
+            m = int(np.prod(self.vshape[vmask], dtype=np.int64))
+            if _use_record_map(self._geom.size, self._dtype.itemsize) and m * new.size < 2 ** 31:
+                # every old record yields m consecutive new records: one record-map
+                # gather with the old packed record staged in LDS
+                per_rec = v2k_copies(self._geom, new, [], vmask)
+                rmap = (copies_to_map(per_rec, m * new.size), ("v2k", vmask.tobytes()) +
+                        self._geom.key() + new.key())
+                return self._repack(None, rmap, newshape, newsplit, newplan, newpadding, new)
+            copies = v2k_copies(self._geom, new, lk, vmask)
+            return self._repack(copies, None, newshape, newsplit, newplan, newpadding, new)
         dense = self._unpack()
         shape_before = self._shape
         bare = False

@@ -227,6 +227,30 @@ class ChunkGeometry(object):
     def chunk_ids(self):
         return list(product(*[range(k) for k in self.nchunks]))
 
+    def combo_layout(self, combo):
+        """Packed addressing of one combination of runs (one run per axis).
+
+        Returns (base, cstr, inner): the packed offset of the combination's
+        first chunk, the packed stride of the chunk index along each axis
+        (linear inside a run: its chunks share one extent), and the C-order
+        strides of a chunk box of the run extents.
+        """
+        n = len(self.vshape)
+        ext = [r[3] for r in combo]
+        base, cstr = 0, []
+        for a, (j0, cnt, st0, ex, co, ce) in enumerate(combo):
+            mult = 1
+            for b in range(a):
+                mult *= ext[b]
+            for b in range(a + 1, n):
+                mult *= self.E[b]
+            base += self.P[a][j0] * mult
+            cstr.append(ex * mult)
+        inner = [1] * n
+        for a in range(n - 2, -1, -1):
+            inner[a] = inner[a + 1] * ext[a + 1]
+        return base, cstr, inner
+
     def copies(self, unpack=False):
         """Strided copies (per record) between the dense record and the packed record.
 
@@ -241,32 +265,142 @@ class ChunkGeometry(object):
             vstride[a] = vstride[a + 1] * self.vshape[a + 1]
         out = []
         for combo in product(*self.runs):
-            shape, dstr, pstr = [], [], []
-            doff, poff = 0, 0
-            ext = [r[3] for r in combo]
+            poff, cstr, inner = self.combo_layout(combo)
+            shape = [r[1] for r in combo] + [(r[5] if unpack else r[3]) for r in combo]
+            dstr = [self.plan[a] * vstride[a] for a in range(n)] + vstride
+            pstr = cstr + inner
+            doff = 0
             for a, (j0, cnt, st0, ex, co, ce) in enumerate(combo):
-                # packed stride of chunk index along a, and base offset
-                mult = 1
-                for b in range(a):
-                    mult *= ext[b]
-                for b in range(a + 1, n):
-                    mult *= self.E[b]
-                poff += self.P[a][j0] * mult
-                shape.append(cnt)
-                dstr.append(self.plan[a] * vstride[a])
-                pstr.append(ex * mult)
                 doff += (st0 + (co if unpack else 0)) * vstride[a]
-            inner = [1] * n
-            for a in range(n - 2, -1, -1):
-                inner[a] = inner[a + 1] * ext[a + 1]
-            for a, (j0, cnt, st0, ex, co, ce) in enumerate(combo):
-                shape.append(ce if unpack else ex)
-                dstr.append(vstride[a])
-                pstr.append(inner[a])
                 if unpack:
                     poff += co * inner[a]
             out.append((shape, dstr, pstr, doff, poff))
         return out
+
+    def record_map(self, unpack=False):
+        """One record's layout change as an int32 gather map (bm_record_gather).
+
+        pack:   map[p] = dense index of packed element p       (len = size)
+        unpack: map[i] = packed index holding dense element i  (len = prod(vshape))
+        Cached.
+        """
+        key = "_map_unpack" if unpack else "_map_pack"
+        m = getattr(self, key, None)
+        if m is None:
+            rec = int(np.prod(self.vshape, dtype=np.int64)) if self.vshape else 1
+            if unpack:
+                m = copies_to_map([(sh, ps, ds, po, do) for sh, ds, ps, do, po in self.copies(True)], rec)
+            else:
+                m = copies_to_map(self.copies(False), self.size)
+            setattr(self, key, m)
+        return m
+
+    def key(self):
+        return (self.vshape, self.plan, self.padding)
+
+
+def copies_to_map(copies, dst_len):
+    """Run strided copies on index arrays: map[dst] = src, as int32.
+
+    copies: (shape, src_strides, dst_strides, src_off, dst_off) in elements.
+    Every destination element must be written exactly by the plan.
+    """
+    m = np.full(dst_len, -1, dtype=np.int64)
+    for shape, ss, ds, so, do in copies:
+        si = np.full((), so, dtype=np.int64)
+        di = np.full((), do, dtype=np.int64)
+        for n, a, b in zip(shape, ss, ds):
+            ax = np.arange(n, dtype=np.int64)
+            si = np.add.outer(si, ax * a)
+            di = np.add.outer(di, ax * b)
+        m[di.reshape(-1)] = si.reshape(-1)
+    assert (m >= 0).all(), "copy plan does not cover the destination"
+    return m.astype(np.int32)
+
+
+def _cstrides(shape):
+    st = [1] * len(shape)
+    for k in range(len(shape) - 2, -1, -1):
+        st[k] = st[k + 1] * int(shape[k + 1])
+    return st
+
+
+def k2v_copies(old, new, kshape, kmask):
+    """keys_to_values (chunk.py:202-289) as strided copies packed -> packed.
+
+    old / new: ChunkGeometry of the value record before / after (new value
+    axes = the moved keys, then the old value axes; moved keys chunked by
+    ``size`` without padding, old value axes keep plan and padding).  kshape:
+    this rank's key extents; kmask: moved keys.  A new chunk's box over the
+    old value axes is exactly an old chunk's padded box (same slices), so
+    every new chunk is a stack of old chunk boxes, one per moved-key index:
+    each byte is read once from the old packing and written once.
+    Entries: (shape, src_strides, dst_strides, src_off, dst_off) in elements.
+    """
+    ks_old = [k * old.size for k in _cstrides(kshape)]
+    stat = [i for i in range(len(kshape)) if not kmask[i]]
+    moved = [i for i in range(len(kshape)) if kmask[i]]
+    ks_new = [k * new.size for k in _cstrides([kshape[i] for i in stat])]
+    nk = len(moved)
+    out = []
+    for combo in product(*new.runs):
+        nbase, ncstr, ninner = new.combo_layout(combo)
+        obase, ocstr, oinner = old.combo_layout(combo[nk:])
+        shape, ss, ds = [], [], []
+        for t, i in enumerate(stat):
+            shape.append(kshape[i]); ss.append(ks_old[i]); ds.append(ks_new[t])
+        soff = obase
+        for t, i in enumerate(moved):
+            j0, cnt, st0, ex, co, ce = combo[t]
+            shape.append(cnt); ss.append(new.plan[t] * ks_old[i]); ds.append(ncstr[t])
+            soff += st0 * ks_old[i]
+        for b in range(len(old.vshape)):
+            shape.append(combo[nk + b][1]); ss.append(ocstr[b]); ds.append(ncstr[nk + b])
+        for t, i in enumerate(moved):
+            shape.append(combo[t][3]); ss.append(ks_old[i]); ds.append(ninner[t])
+        for b in range(len(old.vshape)):
+            shape.append(combo[nk + b][3]); ss.append(oinner[b]); ds.append(ninner[nk + b])
+        out.append((shape, ss, ds, soff, nbase))
+    return out
+
+
+def v2k_copies(old, new, kshape, vmask):
+    """values_to_keys (chunk.py:291-347) as strided copies packed -> packed.
+
+    The moved value axes become trailing keys: a new record (key, b) takes,
+    along each moved axis, row b of the core of the old chunk that owns b
+    (removepad, chunk.py:305-312), and along the remaining value axes the
+    old chunks' padded boxes unchanged (same plan and padding).  new: the
+    ChunkGeometry over the remaining value axes.
+    """
+    nv = len(old.vshape)
+    moved = [a for a in range(nv) if vmask[a]]
+    rest = [a for a in range(nv) if not vmask[a]]
+    mshape = [old.vshape[a] for a in moved]
+    ks_old = [k * old.size for k in _cstrides(kshape)]
+    nks = [k * new.size for k in _cstrides(list(kshape) + mshape)]
+    nkey = len(kshape)
+    out = []
+    for combo in product(*old.runs):
+        obase, ocstr, oinner = old.combo_layout(combo)
+        nbase, ncstr, ninner = new.combo_layout(tuple(combo[a] for a in rest))
+        shape, ss, ds = [], [], []
+        for i in range(nkey):
+            shape.append(kshape[i]); ss.append(ks_old[i]); ds.append(nks[i])
+        soff, doff = obase, nbase
+        for t, a in enumerate(moved):
+            j0, cnt, st0, ex, co, ce = combo[a]
+            shape.append(cnt); ss.append(ocstr[a]); ds.append(old.plan[a] * nks[nkey + t])
+            soff += co * oinner[a]
+            doff += j0 * old.plan[a] * nks[nkey + t]
+        for t, a in enumerate(rest):
+            shape.append(combo[a][1]); ss.append(ocstr[a]); ds.append(ncstr[t])
+        for t, a in enumerate(moved):
+            shape.append(combo[a][5]); ss.append(oinner[a]); ds.append(nks[nkey + t])
+        for t, a in enumerate(rest):
+            shape.append(combo[a][3]); ss.append(oinner[a]); ds.append(ninner[t])
+        out.append((shape, ss, ds, soff, doff))
+    return out
 
 
 # --------------------------------------------------------------------------

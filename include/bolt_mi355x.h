@@ -118,6 +118,20 @@ int bm_gather_rows(const void *src, void *dst, int64_t n_outer, int64_t src_rows
                    int64_t row_bytes, const int64_t *idx, int64_t n_idx, void *stream);
 
 /*
+ * bm_record_gather -- dst[r*dst_rec + o] = src[r*src_rec + map[o]] for
+ * r < nrec, o < dst_rec (sizes in elements of elem_bytes = 1/2/4/8).
+ * map is a DEVICE array of dst_rec int32 indices in [0, src_rec), shared by
+ * every record.  The pack and unpack of ChunkedArray for small records:
+ *   pack   ChunkedArray._chunk flatMap     bolt/spark/chunk.py:131-142
+ *          (map: packed chunk element -> dense value index, halos included)
+ *   unpack ChunkedArray.unchunk/removepad  bolt/spark/chunk.py:146-200, :514-550
+ *          (map: dense value index -> packed element of its chunk's core)
+ * A source record of <= 64 KiB is staged whole in LDS; bit-exact.
+ */
+int bm_record_gather(const void *src, void *dst, int64_t nrec, int64_t src_rec,
+                     int64_t dst_rec, const int32_t *map, int elem_bytes, void *stream);
+
+/*
  * Reductions over a C-contiguous array viewed as [O][R][I]: the middle axis
  * (R records) is reduced, O*I outputs are produced in [O][I] order.  This is
  * the aligned layout that BoltArraySpark._align (array.py:85-115) builds

@@ -60,6 +60,16 @@ class CpuBackend(object):
         d = _np(dst)[dst_off:dst_off + n_outer * idx.size * row_bytes].reshape(n_outer, idx.size, row_bytes)
         d[...] = s[:, idx, :]
 
+    def record_gather(self, src, src_off, dst, dst_off, nrec, src_rec, dst_rec, rmap, key, es):
+        if nrec == 0:
+            return
+        rmap = np.asarray(rmap, dtype=np.int64)
+        assert rmap.size == dst_rec and rmap.min() >= 0 and rmap.max() < src_rec
+        dt = np.dtype((np.void, es))
+        s = _np(src)[src_off:src_off + nrec * src_rec * es].view(dt).reshape(nrec, src_rec)
+        d = _np(dst)[dst_off:dst_off + nrec * dst_rec * es].view(dt).reshape(nrec, dst_rec)
+        d[...] = s[:, rmap]
+
     def permute(self, src, shape, perm, es, dst):
         a = _np(src).view(np.dtype((np.void, es))).reshape(tuple(shape))
         out = _np(dst).view(np.dtype((np.void, es)))

@@ -55,6 +55,11 @@ def test_argument_errors(lib):
     assert lib.bm_gather_rows(None, None, 1, 4, 8, None, 3, None) == -1
     assert b"null pointer" in lib.bm_last_error()
     assert lib.bm_gather_rows(None, None, 0, 4, 8, None, 3, None) == 0  # nothing to move
+    assert lib.bm_record_gather(None, None, 4, 8, 8, None, 16, None) == -1
+    assert b"bad arguments" in lib.bm_last_error()
+    assert lib.bm_record_gather(None, None, 4, 8, 8, None, 8, None) == -1
+    assert b"null pointer" in lib.bm_last_error()
+    assert lib.bm_record_gather(None, None, 0, 8, 8, None, 8, None) == 0  # nothing to move
 
 
 def test_workspace_and_state_sizes(lib):

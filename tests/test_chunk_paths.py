@@ -1,0 +1,123 @@
+"""Chunk pack / unpack: the record-map gather (bm_record_gather, small records)
+against the strided-copy path (one bm_copy_strided per run of equal chunks)
+and against the reference's chunk slicing restated with numpy
+(getslices + removepad, bolt/spark/chunk.py:87-144, :514-618).
+
+Runs on the CPU test executor and (marker `gpu`) through the C ABI on the
+GPU.  Bit-exact: packed bytes of both paths are identical, every chunk equals
+the reference's padded slice, and unchunk restores the input.
+"""
+import numpy as np
+import pytest
+
+import bolt_amd as bolt
+from bolt_amd.mi355x import chunk as chunk_mod
+from bolt_amd.mi355x.plan import getslices
+
+CASES = [
+    # (shape, split, dtype, size, padding)
+    ((6, 64, 64), 1, np.float64, (16, 16), 2),      # C5's record geometry
+    ((5, 20, 30), 1, np.float32, (7, 9), (1, 3)),   # ragged + asymmetric halos
+    ((4, 3, 33, 17), 2, np.uint8, (5, 4), 2),       # 1-byte elements, odd record size
+    ((7, 50, 11), 1, np.uint16, (8, 11), (3, 0)),   # an unchunked axis
+    ((3, 2, 9, 8, 10), 2, np.int32, (4, 3, 5), 1),  # 3 value axes
+    ((9, 100), 1, np.float64, (10,), 4),            # 1 value axis
+    ((2, 128, 64), 1, np.float32, (128, 64), 0),    # one chunk: plan = vshape
+    ((3, 4, 4), 1, np.complex128, (2, 2), 1),       # 16-B elements: strided path only
+]
+
+
+def _rand(shape, dtype, seed):
+    rng = np.random.default_rng(seed)
+    n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    return rng.integers(0, 256, size=n, dtype=np.uint8).view(dtype).reshape(shape)
+
+
+def _expected_chunks(x, split, plan, padding):
+    """(key + chunk id, padded chunk) in key order, as chunk.py:131-142 emits them."""
+    from itertools import product
+    vshape = x.shape[split:]
+    slices = getslices(plan, padding, vshape)
+    out = []
+    for key in np.ndindex(*x.shape[:split]):
+        v = x[key]
+        for cid in product(*[range(len(s)) for s in slices]):
+            out.append((tuple(key) + cid, v[tuple(s[i] for s, i in zip(slices, cid))]))
+    return out
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_record_map_matches_strided_copies(bctx, case, monkeypatch):
+    shape, split, dtype, size, padding = CASES[case]
+    x = _rand(shape, dtype, case)
+    b = bolt.array(x, bctx, axis=tuple(range(split)))
+    packs = {}
+    for use_map in (True, False):
+        monkeypatch.setenv("BOLT_AMD_RECORD_MAP", "1" if use_map else "0")
+        c = b.chunk(size, padding=padding)
+        packs[use_map] = c
+        assert np.asarray(c.unchunk().toarray()).tobytes() == x.tobytes()
+    a, s = packs[True], packs[False]
+    assert bytes(a._packed.cpu().numpy()) == bytes(s._packed.cpu().numpy())
+    want = _expected_chunks(x, split, tuple(int(p) for p in a.plan), tuple(int(p) for p in a.padding))
+    got = list(a.records())
+    assert len(got) == len(want)
+    for (gk, gv), (wk, wv) in zip(got, want):
+        assert gk == wk and gv.shape == wv.shape and gv.tobytes() == np.ascontiguousarray(wv).tobytes()
+
+
+def test_record_map_threshold():
+    assert chunk_mod._use_record_map(8192, 8)          # 64 KiB: staged in LDS
+    assert not chunk_mod._use_record_map(8193, 8)      # larger: strided copies
+    assert not chunk_mod._use_record_map(4, 16)        # 16-B elements: strided copies
+
+
+def test_record_map_inverse():
+    from bolt_amd.mi355x.plan import ChunkGeometry
+    g = ChunkGeometry((20, 30), (7, 9), (1, 3))
+    pm, um = g.record_map(unpack=False), g.record_map(unpack=True)
+    assert pm.size == g.size and um.size == 600
+    # unpack reads, for each dense cell, a packed cell that pack filled from that same dense cell
+    assert np.array_equal(pm[um], np.arange(600))
+
+
+RECHUNK = [
+    # (shape, split, chunk size, padding, op, axes, k2v size)
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "k2v", (2,), None),        # trailing key
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "k2v", (0,), None),        # leading key
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "k2v", (0, 2), None),      # two keys, not adjacent
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "k2v", (1,), (2,)),        # ragged key chunks (5 = 2+2+1)
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "k2v", (0, 1, 2), (3, 2, 4)),
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "v2k", (0,), None),
+    ((4, 5, 6, 20, 30), 3, (7, 9), (1, 3), "v2k", (1,), None),
+    ((3, 9, 8, 10), 1, (4, 3, 5), (1, 1, 2), "v2k", (0, 2), None),
+    ((3, 9, 8, 10), 1, (4, 3, 5), (1, 1, 2), "k2v", (0,), None),
+    ((2, 3, 70, 300), 2, (16, 64), (2, 5), "v2k", (0,), None),       # old record > 64 KiB: strided copies
+    ((2, 3, 70, 300), 2, (16, 64), (2, 5), "v2k", (1,), None),
+]
+
+
+@pytest.mark.parametrize("case", range(len(RECHUNK)))
+@pytest.mark.parametrize("dtype", [np.float64, np.uint8])
+def test_fused_rechunk_matches_dense_path(bctx, case, dtype, monkeypatch):
+    """keys_to_values / values_to_keys packed -> packed equals unpack -> permute -> pack."""
+    shape, split, size, padding, op, axes, ksize = RECHUNK[case]
+    x = _rand(shape, dtype, 100 + case)
+    b = bolt.array(x, bctx, axis=tuple(range(split)))
+    c = b.chunk(size, padding=padding)
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("BOLT_AMD_FUSED_RECHUNK", fused)
+        res[fused] = c.keys_to_values(axes, size=ksize) if op == "k2v" else c.values_to_keys(axes)
+    f, d = res["1"], res["0"]
+    assert f.shape == d.shape and f.split == d.split
+    assert np.array_equal(f.plan, d.plan) and np.array_equal(f.padding, d.padding)
+    assert bytes(f._packed.cpu().numpy()) == bytes(d._packed.cpu().numpy())
+    # and the content is the permuted array
+    if op == "k2v":
+        ks = [i for i in range(split) if i not in axes] + list(axes)
+        perm = ks + list(range(split, len(shape)))
+    else:
+        vs = [split + a for a in axes] + [split + a for a in range(len(shape) - split) if a not in axes]
+        perm = list(range(split)) + vs
+    assert np.asarray(f.unchunk().toarray()).tobytes() == np.ascontiguousarray(x.transpose(perm)).tobytes()

@@ -25,6 +25,7 @@ def timed(f, reps=5):
     out = None
     e0.record()
     for _ in range(reps):
+        out = None  # free the previous result first: one live output, no allocator churn
         out = f()
     e1.record()
     e1.synchronize()
@@ -55,12 +56,18 @@ def main():
         res[name + " unchunk"] = {"ms": round(ms, 3), "GB/s": round((N + P) / ms / 1e6, 1)}
         assert torch.equal(u._data, b._data)
         if pad:
-            ms, _ = timed(lambda: c.keys_to_values((2,)), reps=2)
-            res[name + " keys_to_values((2,))"] = {"ms": round(ms, 3)}
-            ms, _ = timed(lambda: c.values_to_keys((0,)), reps=2)
-            res[name + " values_to_keys((0,))"] = {"ms": round(ms, 3)}
+            # minimum bytes of a re-chunk: read the old packing, write the new one
+            ms, k = timed(lambda: c.keys_to_values((2,)), reps=2)
+            res[name + " keys_to_values((2,))"] = {"ms": round(ms, 3),
+                                                   "GB/s": round((P + k._packed.numel()) / ms / 1e6, 1)}
+            del k
+            ms, v = timed(lambda: c.values_to_keys((0,)), reps=2)
+            res[name + " values_to_keys((0,))"] = {"ms": round(ms, 3),
+                                                   "GB/s": round((P + v._packed.numel()) / ms / 1e6, 1)}
+            del v
         del b, c, u
         torch.cuda.empty_cache()
+    res["record_map"] = os.environ.get("BOLT_AMD_RECORD_MAP", "1")
     print(json.dumps(res, indent=1))
 
 
