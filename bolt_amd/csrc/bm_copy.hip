@@ -44,7 +44,6 @@ constexpr int kThreads = 256;
 #endif
 constexpr int kRcThreads = BM_RC_THREADS;
 constexpr int kUnroll = BM_RC_UNROLL;
-constexpr int kArea = 4096;  // transpose tile = TA x (kArea / TA) elements
 
 // ---------------------------------------------------------------- rowcopy --
 template <int VB>
@@ -89,20 +88,30 @@ struct TransDesc {
   Decomp batch;    // remaining dims
 };
 
-// TA: tile extent along a (TB = kArea / TA along b), chosen on the host to
-// fit the two extents (a 32-wide source axis gets 32 x 128 tiles, not half-
-// empty 64 x 64 ones).  VA / VB: elements per lane for the global load
-// (along a) / store (along b).
-template <typename T, int TA, int VA, int VB>
+// TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
+// destination-contiguous dim), chosen on the host per element size and
+// extents (pick_tile).  VA / VB: elements per lane for the global load
+// (along a) / store (along b).  Every load of a tile is issued before the
+// first LDS write, so a block keeps TB*TA*sizeof(T) bytes in flight
+// (tools/microbench/transpose_tiles.hip: +6% at 64x256 f32 over writing
+// each load to LDS as it lands).
+template <typename T, int TA, int TB, int VA, int VB>
 __global__ void __launch_bounds__(kThreads)
     k_transpose(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
-  constexpr int TB = kArea / TA;
   __shared__ T tile[TB][TA + 1];
   constexpr int NVA = TA / VA;
   constexpr int RPA = kThreads / NVA;
   constexpr int NVB = TB / VB;
-  static_assert(RPA <= TB && kThreads / NVB <= TA, "tile too small for the thread layout");
   constexpr int RPB = kThreads / NVB;
+  static_assert(NVA <= kThreads && NVB <= kThreads, "tile row wider than the block");
+  static_assert(RPA <= TB && RPB <= TA && TB % RPA == 0 && TA % RPB == 0, "tile too small for the thread layout");
+  constexpr int NL = TB / RPA;
+  constexpr int NS = TA / RPB;
+  // loads in flight per lane: all of them, up to 16 registers' worth (unaligned
+  // element-wise loads go in batches instead of spilling)
+  constexpr int RPL = (VA * (int)sizeof(T) + 3) / 4;  // VGPRs per load
+  constexpr int NLB = (NL * RPL <= 64) ? NL : (16 / RPL > 0 ? 16 / RPL : 1);
+  static_assert(NL % NLB == 0, "load batch must divide the loads");
   const int tx = threadIdx.x % NVA, ty = threadIdx.x / NVA;
   const int ux = threadIdx.x % NVB, uy = threadIdx.x / NVB;
   const int ia = tx * VA;
@@ -119,24 +128,30 @@ __global__ void __launch_bounds__(kThreads)
     decomp2(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
 
-    // load: lanes walk dim a (source-contiguous)
+    // load: lanes walk dim a (source-contiguous); all loads in flight first
     const T *s = src + so + a0 + b0 * d.sb;
     const bool fullA = (a0 + ia + VA <= d.La);
 #pragma unroll
-    for (int it = 0; it < TB / RPA; ++it) {
-      const int rb = ty + it * RPA;
-      if (b0 + rb < d.Lb) {
-        const T *p = s + ia + (int64_t)rb * d.sb;
-        if (fullA) {
-          T v[VA];
-          vload_nt<T, VA>(p, v);
+    for (int i0 = 0; i0 < NL; i0 += NLB) {
+      T v[NLB][VA];
 #pragma unroll
-          for (int k = 0; k < VA; ++k) tile[rb][ia + k] = v[k];
-        } else {
+      for (int j = 0; j < NLB; ++j) {
+        const int rb = ty + (i0 + j) * RPA;
+        if (b0 + rb < d.Lb) {
+          const T *p = s + ia + (int64_t)rb * d.sb;
+          if (fullA) {
+            vload_nt<T, VA>(p, v[j]);
+          } else {
 #pragma unroll
-          for (int k = 0; k < VA; ++k)
-            if (a0 + ia + k < d.La) tile[rb][ia + k] = p[k];
+            for (int k = 0; k < VA; ++k) v[j][k] = (a0 + ia + k < d.La) ? p[k] : T(0);
+          }
         }
+      }
+#pragma unroll
+      for (int j = 0; j < NLB; ++j) {
+        const int rb = ty + (i0 + j) * RPA;
+#pragma unroll
+        for (int k = 0; k < VA; ++k) tile[rb][ia + k] = v[j][k];
       }
     }
     __syncthreads();
@@ -145,19 +160,19 @@ __global__ void __launch_bounds__(kThreads)
     T *q = dst + dof + b0 + a0 * d.da;
     const bool fullB = (b0 + ib + VB <= d.Lb);
 #pragma unroll
-    for (int it = 0; it < TA / RPB; ++it) {
+    for (int it = 0; it < NS; ++it) {
       const int ra = uy + it * RPB;
       if (a0 + ra < d.La) {
-        T v[VB];
+        T w[VB];
 #pragma unroll
-        for (int k = 0; k < VB; ++k) v[k] = tile[ib + k][ra];
+        for (int k = 0; k < VB; ++k) w[k] = tile[ib + k][ra];
         T *p = q + (int64_t)ra * d.da + ib;
         if (fullB) {
-          vstore_nt<T, VB>(p, v);
+          vstore_nt<T, VB>(p, w);
         } else {
 #pragma unroll
           for (int k = 0; k < VB; ++k)
-            if (b0 + ib + k < d.Lb) p[k] = v[k];
+            if (b0 + ib + k < d.Lb) p[k] = w[k];
         }
       }
     }
@@ -315,47 +330,79 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   return BM_OK;
 }
 
-template <typename T, int TA>
-void launch_transpose_ta(const T *src, T *dst, const TransDesc &td, bool va_vec, bool vb_vec, int grid,
-                         hipStream_t st) {
+template <typename T, int TA, int TB>
+void launch_transpose_tile(const T *src, T *dst, const TransDesc &td, bool va_vec, bool vb_vec, int grid,
+                           hipStream_t st) {
   constexpr int W = 16 / (int)sizeof(T);
   if (va_vec && vb_vec)
-    k_transpose<T, TA, W, W><<<grid, kThreads, 0, st>>>(src, dst, td);
+    k_transpose<T, TA, TB, W, W><<<grid, kThreads, 0, st>>>(src, dst, td);
   else if (va_vec)
-    k_transpose<T, TA, W, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+    k_transpose<T, TA, TB, W, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
   else if (vb_vec)
-    k_transpose<T, TA, 1, W><<<grid, kThreads, 0, st>>>(src, dst, td);
+    k_transpose<T, TA, TB, 1, W><<<grid, kThreads, 0, st>>>(src, dst, td);
   else
-    k_transpose<T, TA, 1, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
+    k_transpose<T, TA, TB, 1, 1><<<grid, kThreads, 0, st>>>(src, dst, td);
 }
 
+// Tile shapes per element size (TA x TB elements).  Measured on the C2 swap
+// shape with 1 MiB source rows (tools/microbench/transpose_tiles.hip,
+// profiles/r01_tt2.log): 128-256-B source segments and ~1-2 KiB destination
+// segments per tile row are fastest; the others serve short extents.
+struct Tile { int ta, tb; };
+constexpr Tile kTiles1[] = {{128, 256}, {128, 128}, {64, 64}, {256, 64}, {64, 256}};
+constexpr Tile kTiles2[] = {{128, 256}, {64, 256}, {64, 64}, {128, 64}, {256, 32}, {32, 256}};
+constexpr Tile kTiles4[] = {{64, 256}, {32, 256}, {64, 64}, {64, 128}, {128, 32}, {256, 16}, {16, 256}, {32, 64}};
+constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {32, 64}, {64, 64}, {64, 32}, {128, 16}, {16, 128}};
+
 template <typename T>
-int launch_transpose_t(const T *src, T *dst, const TransDesc &td, int ta, bool va_vec, bool vb_vec,
+int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool va_vec, bool vb_vec,
                        hipStream_t st) {
   uint64_t g = td.ntiles;
   if (g > 0x7fffffffull) g = 0x7fffffffull;
   const int grid = (int)g;
-  switch (ta) {
-    case 16: launch_transpose_ta<T, 16>(src, dst, td, va_vec, vb_vec, grid, st); break;
-    case 32: launch_transpose_ta<T, 32>(src, dst, td, va_vec, vb_vec, grid, st); break;
-    case 128: launch_transpose_ta<T, 128>(src, dst, td, va_vec, vb_vec, grid, st); break;
-    case 256: launch_transpose_ta<T, 256>(src, dst, td, va_vec, vb_vec, grid, st); break;
-    default: launch_transpose_ta<T, 64>(src, dst, td, va_vec, vb_vec, grid, st); break;
+#define BM_TILE(A, B) \
+  if (tl.ta == A && tl.tb == B) { launch_transpose_tile<T, A, B>(src, dst, td, va_vec, vb_vec, grid, st); return BM_OK; }
+  if constexpr (sizeof(T) == 1) {
+    BM_TILE(128, 256) BM_TILE(128, 128) BM_TILE(64, 64) BM_TILE(256, 64) BM_TILE(64, 256)
+  } else if constexpr (sizeof(T) == 2) {
+    BM_TILE(128, 256) BM_TILE(64, 256) BM_TILE(64, 64) BM_TILE(128, 64) BM_TILE(256, 32) BM_TILE(32, 256)
+  } else if constexpr (sizeof(T) == 4) {
+    BM_TILE(64, 256) BM_TILE(32, 256) BM_TILE(64, 64) BM_TILE(64, 128) BM_TILE(128, 32) BM_TILE(256, 16)
+    BM_TILE(16, 256) BM_TILE(32, 64)
+  } else {
+    BM_TILE(32, 256) BM_TILE(16, 256) BM_TILE(32, 64) BM_TILE(64, 64) BM_TILE(64, 32) BM_TILE(128, 16)
+    BM_TILE(16, 128)
   }
-  return BM_OK;
+#undef BM_TILE
+  bm_set_error("bm_copy_strided: no transpose tile %dx%d for %d-byte elements", tl.ta, tl.tb, (int)sizeof(T));
+  return BM_E_ARG;
 }
 
-// Tile shape with the least padding waste for extents (La, Lb); ties keep 64x64.
-int pick_tile_a(int64_t La, int64_t Lb) {
-  const int cands[5] = {64, 32, 128, 16, 256};
-  int best = 64;
+// Relative cost of a tile row segment of n bytes (1.0 = the fastest shape),
+// from the same sweep: short segments waste DRAM bursts.
+double seg_cost_read(int64_t n) { return n >= 256 ? 1.0 : n >= 128 ? 1.02 : n >= 64 ? 1.25 : 1.6; }
+double seg_cost_write(int64_t n) { return n >= 1024 ? 1.0 : n >= 512 ? 1.05 : n >= 256 ? 1.06 : n >= 128 ? 1.3 : 1.6; }
+
+// The tile with the least estimated time for extents (La, Lb): padded tile
+// traffic x segment costs.
+Tile pick_tile(int64_t La, int64_t Lb, int es) {
+  const Tile *c;
+  int n;
+  switch (es) {
+    case 1: c = kTiles1; n = sizeof(kTiles1) / sizeof(Tile); break;
+    case 2: c = kTiles2; n = sizeof(kTiles2) / sizeof(Tile); break;
+    case 4: c = kTiles4; n = sizeof(kTiles4) / sizeof(Tile); break;
+    default: c = kTiles8; n = sizeof(kTiles8) / sizeof(Tile); break;
+  }
+  Tile best = c[0];
   double best_w = 1e300;
-  for (int ta : cands) {
-    const int tb = kArea / ta;
-    const double w = (double)(((La + ta - 1) / ta) * ta) * (double)(((Lb + tb - 1) / tb) * tb);
-    if (w < best_w * 0.97) {  // a new shape must save >3% of the tile traffic
+  for (int i = 0; i < n; ++i) {
+    const int64_t ta = c[i].ta, tb = c[i].tb;
+    const double pa = (double)(((La + ta - 1) / ta) * ta), pb = (double)(((Lb + tb - 1) / tb) * tb);
+    const double w = pa * pb * seg_cost_read(std::min(ta, La) * es) * seg_cost_write(std::min(tb, Lb) * es);
+    if (w < best_w * 0.999) {
       best_w = w;
-      best = ta;
+      best = c[i];
     }
   }
   return best;
@@ -376,8 +423,8 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
     return BM_E_ARG;
   }
-  const int TA = pick_tile_a(td.La, td.Lb);
-  const int TB = kArea / TA;
+  const Tile tl = pick_tile(td.La, td.Lb, es);
+  const int TA = tl.ta, TB = tl.tb;
   const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);
   const uint64_t ntB = (uint64_t)((td.Lb + TB - 1) / TB);
   uint64_t nb = 1;
@@ -393,10 +440,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     if (k != b && (dims[k].ds * es) % 16) vb = false;
   }
   switch (es) {
-    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, TA, va, vb, st);
-    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, TA, va, vb, st);
-    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, TA, va, vb, st);
-    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, TA, va, vb, st);
+    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, st);
+    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, st);
+    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, st);
+    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, st);
     default: break;
   }
   bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);
