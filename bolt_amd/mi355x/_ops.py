@@ -50,6 +50,8 @@ class HipBackend(object):
     def __init__(self):
         self.lib = _lib.load()
         self._maps = {}  # (device, geometry key) -> resident int32 record map
+        self._args = {}  # (shape, perm) -> ctypes arguments of bm_permute
+        self._ws = {}    # reduction -> workspace bytes
 
     @staticmethod
     def _stream(t):
@@ -71,8 +73,14 @@ class HipBackend(object):
                    "bm_copy_strided")
 
     def permute(self, src, shape, perm, es, dst):
-        _lib.check(self.lib.bm_permute(self._ptr(src), self._ptr(dst), len(shape),
-                                       _lib.i64_array(shape), _lib.i32_array(perm), int(es),
+        key = (tuple(shape), tuple(perm))
+        args = self._args.get(key)
+        if args is None:
+            args = (len(shape), _lib.i64_array(shape), _lib.i32_array(perm))
+            if len(self._args) > 4096:
+                self._args.clear()
+            self._args[key] = args
+        _lib.check(self.lib.bm_permute(self._ptr(src), self._ptr(dst), args[0], args[1], args[2], int(es),
                                        self._stream(src)), "bm_permute")
 
     def gather_rows(self, src, src_off, dst, dst_off, n_outer, src_rows, row_bytes, idx):
@@ -111,12 +119,16 @@ class HipBackend(object):
 
     def _workspace(self, stat, code, O, R, I, device):
         import torch
-        n = ctypes.c_size_t(0)
-        _lib.check(self.lib.bm_reduce_workspace_bytes(stat, code, O, R, I, ctypes.byref(n)),
-                   "bm_reduce_workspace_bytes")
-        if n.value == 0:
+        key = (stat, code, O, R, I)
+        nb = self._ws.get(key)
+        if nb is None:
+            n = ctypes.c_size_t(0)
+            _lib.check(self.lib.bm_reduce_workspace_bytes(stat, code, O, R, I, ctypes.byref(n)),
+                       "bm_reduce_workspace_bytes")
+            nb = self._ws[key] = n.value
+        if nb == 0:
             return None, 0
-        return torch.empty(n.value, dtype=torch.uint8, device=device), n.value
+        return torch.empty(nb, dtype=torch.uint8, device=device), nb
 
     def reduce(self, stat, src, code, O, R, I, out, out_code):
         ws, nws = self._workspace(stat, code, O, R, I, src.device)

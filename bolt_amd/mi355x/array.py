@@ -55,6 +55,11 @@ def _check_swap_plan(vshape, dtype, size):
         raise type(err)(*err.args)
 
 
+_SWAP_PLANS = {}   # (shape, split, dtype, kaxes, vaxes, size) -> (perm, newsplit) | _NOOP
+_NOOP = object()
+_REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
+
+
 class BoltArrayMI355X(BoltArray):
 
     _metadata = {
@@ -231,6 +236,28 @@ class BoltArrayMI355X(BoltArray):
         chunking; it is validated the same way (getplan + _chunk checks) and
         does not change the result.  Executed as one permute kernel.
         """
+        try:  # host plan of an already validated (shape, split, dtype, axes, size)
+            key = (self._shape, self._split, self._dtype, tuple(int(k) for k in tupleize(kaxes)),
+                   tuple(int(v) for v in tupleize(vaxes)), size if type(size) is str else tupleize(size))
+            hash(key)
+        except (TypeError, ValueError):
+            key = None
+        hit = _SWAP_PLANS.get(key) if key is not None else None
+        if hit is not None:
+            if hit is _NOOP:
+                return self
+            return self._permute(*hit)
+        plan = self._swap_plan(kaxes, vaxes, size)
+        if key is not None:
+            if len(_SWAP_PLANS) > 4096:
+                _SWAP_PLANS.clear()
+            _SWAP_PLANS[key] = _NOOP if plan is None else plan
+        if plan is None:
+            return self
+        return self._permute(*plan)
+
+    def _swap_plan(self, kaxes, vaxes, size):
+        """Validation and net permutation of swap: (perm, newsplit), or None for a no-op."""
         kaxes = np.asarray(tupleize(kaxes), 'int')
         vaxes = np.asarray(tupleize(vaxes), 'int')
         if type(size) is not str:
@@ -241,7 +268,7 @@ class BoltArrayMI355X(BoltArray):
                              'end up with all data on a single key')
 
         if len(kaxes) == 0 and len(vaxes) == 0:
-            return self
+            return None
 
         # the chunk plan the reference would build (errors surface the same way)
         if not (self._split == self.ndim):
@@ -258,8 +285,7 @@ class BoltArrayMI355X(BoltArray):
         kaxes = [int(k) % self._split for k in kaxes]
         vaxes = [int(v) % nv for v in vaxes] if nv else []
 
-        perm, newsplit = swap_perm(self.ndim, self._split, kaxes, vaxes)
-        return self._permute(perm, newsplit)
+        return swap_perm(self.ndim, self._split, kaxes, vaxes)
 
     def transpose(self, *axes):
         """Permute the axes, split unchanged (array.py:765-808)."""
@@ -518,29 +544,34 @@ class BoltArrayMI355X(BoltArray):
         if the reduced axes are not one block they are first permuted to the
         front (what _align's swap does physically, array.py:85-115).
         """
-        axset = sorted(set(int(a) for a in axis))
-        kept = [i for i in range(self.ndim) if i not in axset]
-        out_shape = tuple(self._shape[i] for i in kept)
-        if stat in (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN):
-            out_dtype = self._dtype
-        else:
-            out_dtype = stat_dtype(self._dtype, out_shape)
-        code = dtype_code(self._dtype)
-        ocode = dtype_code(out_dtype)
-        be = self._backend
         ctx = self._ctx
+        lshape = self._local_shape
+        pkey = (lshape, tuple(axis), stat, self._dtype, self._shape, ctx.world_size)
+        plan = _REDUCE_PLANS.get(pkey)
+        if plan is None:
+            axset = sorted(set(int(a) for a in axis))
+            kept = [i for i in range(self.ndim) if i not in axset]
+            out_shape = tuple(self._shape[i] for i in kept)
+            if stat in (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN):
+                out_dtype = self._dtype
+            else:
+                out_dtype = stat_dtype(self._dtype, out_shape)
+            perm, O, R, I = reduce_layout(lshape, axset)
+            plan = (axset, kept, out_shape, out_dtype, dtype_code(self._dtype), dtype_code(out_dtype),
+                    perm, O, R, I, int(np.prod(lshape, dtype=np.int64)))
+            if len(_REDUCE_PLANS) > 4096:
+                _REDUCE_PLANS.clear()
+            _REDUCE_PLANS[pkey] = plan
+        axset, kept, out_shape, out_dtype, code, ocode, perm, O, R, I, nloc = plan
+        be = self._backend
         dev = self._data.device
         es = self._dtype.itemsize
-
-        lshape = self._local_shape
         src = self._data
-        perm, O, R, I = reduce_layout(lshape, axset)
         if perm is not None:
             tmp = _empty(src.numel(), dev)
             if src.numel():
                 be.permute(src, lshape, perm, es, tmp)
             src = tmp
-        nloc = int(np.prod(lshape, dtype=np.int64))
 
         if ctx.world_size == 1 or 0 not in axset:
             # every output lives on this rank (or this rank's slab of them)
