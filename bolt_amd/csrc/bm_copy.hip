@@ -34,7 +34,11 @@ constexpr int kThreads = 256;
 #define BM_RC_UNROLL 1
 #endif
 #ifndef BM_RC_GRIDCAP
-#define BM_RC_GRIDCAP 1048576  // A/B (profiles/r01_ab3..ab5): one vector per lane, many blocks: +15-25% on C3/C4 swaps
+#define BM_RC_GRIDCAP 16777208  // one vector per lane, a block per 256 vectors, up to the 2^32-thread launch limit
+                                // (profiles/r01_ab3..ab5: many blocks +15-25% on C3/C4 swaps)
+#endif
+#ifndef BM_RC_XCD
+#define BM_RC_XCD 0  // XCD-grouped covering grid: +5% in a C4 microbench (r01_rc1) but -3..-20% in the product A/B (r01_ab_rc)
 #endif
 #ifndef BM_RUNS_T
 #define BM_RUNS_T 1
@@ -43,16 +47,22 @@ constexpr int kThreads = 256;
 #define BM_RUNS_MAXB 64  // A/B (profiles/r01_ab5): +35% at 32-B runs, +4% at 64 B, even at 128 B
 #endif
 constexpr int kRcThreads = BM_RC_THREADS;
+// HIP launch limit: grid * block threads < 2^32
+constexpr uint64_t kMaxGrid = 0xffffffffull / 1024;
 constexpr int kUnroll = BM_RC_UNROLL;
 
 // ---------------------------------------------------------------- rowcopy --
 template <int VB>
 __global__ void __launch_bounds__(kRcThreads)
     k_rowcopy(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
-              FastDiv vpr, uint64_t total, int es) {
+              FastDiv vpr, uint64_t total, int es, int xcd) {
   typedef typename VecB<VB>::t V;
   const uint64_t step = (uint64_t)gridDim.x * kRcThreads * kUnroll;
-  for (uint64_t base = (uint64_t)blockIdx.x * kRcThreads * kUnroll + threadIdx.x;
+  // xcd: the grid covers the copy (a multiple of 8 blocks); blocks dealt to
+  // XCD x (b % 8 under round-robin dispatch) take the x-th contiguous eighth
+  uint64_t bid = blockIdx.x;
+  if (xcd) bid = (bid % 8) * (gridDim.x / 8) + bid / 8;
+  for (uint64_t base = bid * kRcThreads * kUnroll + threadIdx.x;
        base < total; base += step) {
     V reg[kUnroll];
     int64_t doff[kUnroll];
@@ -319,13 +329,23 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   const uint64_t vpr = (uint64_t)(row_bytes / VB);
   const uint64_t total = rows * vpr;
   const FastDiv fv = make_fastdiv(vpr);
-  const int grid = grid_for(total, (uint64_t)kRcThreads * kUnroll, BM_RC_GRIDCAP);
+  const uint64_t per = (uint64_t)kRcThreads * kUnroll;
+  const uint64_t need = (total + per - 1) / per;
+  int grid, xcd = 0;
+  if (BM_RC_XCD && need >= 64 && need <= BM_RC_GRIDCAP) {
+    grid = (int)((need + 7) / 8 * 8);
+    xcd = 1;
+  } else if (need <= BM_RC_GRIDCAP) {
+    grid = (int)std::max<uint64_t>(need, 1);  // one vector per lane
+  } else {
+    grid = grid_for(total, per, BM_RC_GRIDCAP);
+  }
   switch (VB) {
-    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
-    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es); break;
+    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
+    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
+    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
+    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
+    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
   }
   return BM_OK;
 }
@@ -358,7 +378,7 @@ template <typename T>
 int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool va_vec, bool vb_vec,
                        hipStream_t st) {
   uint64_t g = td.ntiles;
-  if (g > 0x7fffffffull) g = 0x7fffffffull;
+  if (g > kMaxGrid) g = kMaxGrid;  // grid-stride beyond the launch limit
   const int grid = (int)g;
 #define BM_TILE(A, B) \
   if (tl.ta == A && tl.tb == B) { launch_transpose_tile<T, A, B>(src, dst, td, va_vec, vb_vec, grid, st); return BM_OK; }
@@ -513,7 +533,7 @@ int try_transpose_runs(const char *src, char *dst, const std::vector<Dim> &dims,
   d.ntAB = make_fastdiv(ntA * ntB);
   d.ntiles = ntA * ntB * nbatch;
   uint64_t g = d.ntiles;
-  if (g > 0x7fffffffull) g = 0x7fffffffull;
+  if (g > kMaxGrid) g = kMaxGrid;
   const uint4 *s = (const uint4 *)src;
   uint4 *t = (uint4 *)dst;
   switch (W) {

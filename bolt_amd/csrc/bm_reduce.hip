@@ -26,6 +26,7 @@
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: grid * block threads < 2^32
 #ifndef BM_ROWS_UNROLL
 #define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
 #endif
@@ -237,6 +238,7 @@ struct ColsDesc {
   int32_t tcv;  // threads across columns (power of two <= 256)
   int32_t nph;  // row phases = 256 / tcv
   FastDiv ntc;  // column tiles per O
+  int64_t tile0;  // first (o, column tile) of this launch (launches split at the grid limit)
 };
 
 template <typename T, int VEC, int MODE>
@@ -244,7 +246,7 @@ __global__ void __launch_bounds__(kThreads)
     k_red_cols(const T *__restrict__ src, ColsDesc d, Sink sk) {
   __shared__ double sm0[kThreads * VEC];
   __shared__ double sm1[(MODE == M_MOM) ? kThreads * VEC : 1];
-  const uint64_t ot = blockIdx.x;
+  const uint64_t ot = (uint64_t)d.tile0 + blockIdx.x;
   const uint64_t o = fd_div(ot, d.ntc);
   const uint64_t tc = ot - o * d.ntc.d;
   const int64_t c = blockIdx.y;
@@ -368,13 +370,14 @@ struct RowsDesc {
   int64_t rchunk;
   FastDiv nchunks;
   int64_t nitems;  // O * nchunks
+  int64_t item0;   // first item of this launch (launches split at the grid limit)
 };
 
 template <typename T, int VEC, int MODE>
 __global__ void __launch_bounds__(kThreads)
     k_red_rows(const T *__restrict__ src, RowsDesc d, Sink sk) {
   const int lane = threadIdx.x & 63;
-  const int64_t item = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const int64_t item = d.item0 + (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   if (item >= d.nitems) return;  // whole wave exits; no block barrier below
   const uint64_t o = fd_div((uint64_t)item, d.nchunks);
   const int64_t c = item - (int64_t)o * (int64_t)d.nchunks.d;
@@ -589,14 +592,17 @@ int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64
     d.nchunks = make_fastdiv((uint64_t)p.nchunks);
     d.nitems = O * p.nchunks;
     const int64_t blocks = cdiv(d.nitems, kThreads / 64);
-    if (blocks > 0x7fffffff) { bm_set_error("bm_reduce: too many rows"); return BM_E_ARG; }
-    const int g = (int)blocks;
-    switch (p.vec) {
+    // one launch per kMaxBlocks blocks (HIP: grid * block threads < 2^32)
+    for (int64_t b0 = 0; b0 < blocks; b0 += kMaxBlocks) {
+      const int g = (int)std::min<int64_t>(kMaxBlocks, blocks - b0);
+      d.item0 = b0 * (kThreads / 64);
+      switch (p.vec) {
 #define BM_ROWS_CASE(V) \
   case V: if constexpr (V * sizeof(T) <= 16) { k_red_rows<T, V, MODE><<<g, kThreads, 0, st>>>(s, d, sk); } break;
-      BM_ROWS_CASE(16) BM_ROWS_CASE(8) BM_ROWS_CASE(4) BM_ROWS_CASE(2)
-      default: k_red_rows<T, 1, MODE><<<g, kThreads, 0, st>>>(s, d, sk); break;
+        BM_ROWS_CASE(16) BM_ROWS_CASE(8) BM_ROWS_CASE(4) BM_ROWS_CASE(2)
+        default: k_red_rows<T, 1, MODE><<<g, kThreads, 0, st>>>(s, d, sk); break;
 #undef BM_ROWS_CASE
+      }
     }
   } else {
     ColsDesc d;
@@ -605,14 +611,17 @@ int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64
     d.tcv = p.tcv; d.nph = p.nph;
     d.ntc = make_fastdiv((uint64_t)p.ntc);
     const int64_t bx = O * p.ntc;
-    if (bx > 0x7fffffff) { bm_set_error("bm_reduce: too many output tiles"); return BM_E_ARG; }
-    dim3 grid((unsigned)bx, (unsigned)p.nchunks);
-    switch (p.vec) {
+    const int64_t per = std::max<int64_t>(1, kMaxBlocks / p.nchunks);
+    for (int64_t t0 = 0; t0 < bx; t0 += per) {
+      d.tile0 = t0;
+      dim3 grid((unsigned)std::min<int64_t>(per, bx - t0), (unsigned)p.nchunks);
+      switch (p.vec) {
 #define BM_COLS_CASE(V) \
   case V: if constexpr (V * sizeof(T) <= 16) { k_red_cols<T, V, MODE><<<grid, kThreads, 0, st>>>(s, d, sk); } break;
-      BM_COLS_CASE(8) BM_COLS_CASE(4) BM_COLS_CASE(2)
-      default: k_red_cols<T, 1, MODE><<<grid, kThreads, 0, st>>>(s, d, sk); break;
+        BM_COLS_CASE(8) BM_COLS_CASE(4) BM_COLS_CASE(2)
+        default: k_red_cols<T, 1, MODE><<<grid, kThreads, 0, st>>>(s, d, sk); break;
 #undef BM_COLS_CASE
+      }
     }
   }
   return BM_OK;

@@ -59,10 +59,12 @@ def normalize(index, shape):
                                  "produce an empty dimension".format(idx, n, size))
             index[n] = slc
         else:
-            adjusted = np.array(idx)
-            inds = np.where(adjusted < 0)
-            adjusted[inds] += size
-            if adjusted.min() < 0 or adjusted.max() > size - 1:
+            adjusted = np.asarray(idx)
+            neg = adjusted < 0
+            if neg.any():  # copy only when negatives wrap
+                adjusted = np.array(adjusted)
+                adjusted[neg] += size
+            if adjusted.size and (adjusted.min() < 0 or adjusted.max() > size - 1):
                 raise ValueError("Index {} out of bounds in dimension {} with "
                                  "shape {}".format(idx, n, size))
             index[n] = adjusted
@@ -83,9 +85,9 @@ def _listify(lst, dim):
     """bolt/utils.py:85-103: integer indices, bounded by dim, flattened."""
     if len(lst) and lst.dtype != int:  # every element of an ndarray shares its dtype
         raise ValueError("indices must be integers")
-    if np.any(np.asarray(lst) >= dim):
+    if len(lst) and np.asarray(lst).max() >= dim:
         raise ValueError("indices out of bounds for axis with size %s" % dim)
-    return lst.flatten()
+    return lst.ravel()
 
 
 def advanced_points(index, shape, split):
@@ -101,7 +103,7 @@ def advanced_points(index, shape, split):
     if not all(i.shape == ishape for i in index):
         raise ValueError("shape mismatch: indexing arrays could not be broadcast "
                          "together with shapes " + ("%s " * len(shape)) % tuple(i.shape for i in index))
-    index = [_listify(i, d).astype(np.int64) for i, d in zip(index, shape)]
+    index = [_listify(i, d).astype(np.int64, copy=False) for i, d in zip(index, shape)]
     n = int(np.prod(ishape, dtype=np.int64))
     kshape, vshape = tuple(shape[:split]), tuple(shape[split:])
     K = np.ravel_multi_index(index[:split], kshape) if split else np.zeros(n, np.int64)
@@ -109,6 +111,10 @@ def advanced_points(index, shape, split):
     vsize = int(np.prod(vshape, dtype=np.int64))
     if n == 0:
         pts = np.zeros(0, np.int64)
+    elif vshape and bool(np.all(K[1:] >= K[:-1])):
+        # keys listed in order: one run per key, already in key order -- the
+        # reference's grouping is the identity (numpy's fancy indexing)
+        pts = K * vsize + V
     else:
         starts = np.flatnonzero(np.r_[True, K[1:] != K[:-1]])
         ends = np.r_[starts[1:], n]

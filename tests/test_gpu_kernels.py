@@ -225,3 +225,24 @@ def test_reduce_state_and_combine_match_single_pass():
         ref = {_lib.STAT_MEAN: x.mean(0), _lib.STAT_VAR: x.var(0), _lib.STAT_STD: x.std(0),
                _lib.STAT_SUM: x.sum(0)}[stat]
         assert np.allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("O,R,I", [(70_000_000, 2, 1), (20_000_000, 2, 3)])
+def test_reduce_beyond_one_launch(O, R, I):
+    """Reductions whose grid exceeds HIP's 2^32-thread launch limit run as
+    several launches (rows: 4 outputs per block, > 16.7M blocks; cols: one
+    column tile per output row)."""
+    import torch
+    from bolt_amd.mi355x import _lib
+    from bolt_amd.mi355x._ops import dtype_code
+    be = _be()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(O + I)
+    x = torch.randint(0, 1000, (O, R, I), generator=g, device="cuda", dtype=torch.int32).float()
+    src = x.view(torch.uint8).reshape(-1)
+    out = torch.empty(O * I * 4, dtype=torch.uint8, device="cuda")
+    be.reduce(_lib.STAT_MEAN, src, dtype_code(np.float32), O, R, I, out, dtype_code(np.float32))
+    want = x.double().mean(dim=1).float().reshape(-1)
+    assert torch.equal(out.view(torch.float32), want)  # small integers: exact in float64, one rounding
+    del x, src, out, want
+    torch.cuda.empty_cache()

@@ -104,6 +104,9 @@ OPS = {
     "runs32": lambda: Permute((4096, 4096, 8), (1, 0, 2), np.float32),
     "runs64": lambda: Permute((4096, 2048, 16), (1, 0, 2), np.float32),
     "runs128": lambda: Permute((2048, 2048, 32), (1, 0, 2), np.float32),
+    "c3_full": lambda: Permute((4096, 256, 256, 32), (1, 2, 0, 3), np.float32),
+    "t64_swap": lambda: Permute((8192, 256, 256, 32), (1, 2, 0, 3), np.float32),
+    "c4_full": lambda: Permute((10000, 1024, 1024), (1, 0, 2), np.uint16),
     "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
     "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
     "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),

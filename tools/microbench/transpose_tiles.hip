@@ -75,7 +75,7 @@ void launch_v(const void* src, void* dst, int64_t La, int64_t Lb) {
 template <typename T, int TA, int TB, int THREADS>
 Variant V() {
   Variant v;
-  snprintf(v.name, sizeof v.name, "es%d %3dx%-4d t%d (%4dB rd, %4dB wr, %2dKB)", (int)sizeof(T), TA, TB, THREADS,
+  snprintf(v.name, sizeof v.name, "es%d %3dx%-4d t%-4d (%4dB rd, %4dB wr, %2dKB)", (int)sizeof(T), TA, TB, THREADS,
            TA * (int)sizeof(T), TB * (int)sizeof(T), (int)(TA * TB * sizeof(T) / 1024));
   v.es = sizeof(T);
   v.launch = &launch_v<T, TA, TB, THREADS>;
@@ -92,14 +92,11 @@ int main() {
   for (int64_t i = 0; i < nbytes; ++i) h[i] = (uint8_t)((i * 2654435761ull) >> 13);
   CK(hipMemcpy(src, h.data(), nbytes, hipMemcpyHostToDevice));
   std::vector<Variant> vs = {
-      V<uint8_t, 64, 64, 256>(),   V<uint8_t, 128, 128, 256>(), V<uint8_t, 128, 256, 256>(),
-      V<uint8_t, 64, 512, 256>(),  V<uint8_t, 128, 512, 256>(), V<uint8_t, 256, 128, 256>(),
-      V<uint16_t, 64, 64, 256>(),  V<uint16_t, 64, 256, 256>(), V<uint16_t, 64, 512, 256>(),
-      V<uint16_t, 128, 256, 256>(), V<uint16_t, 32, 512, 256>(), V<uint16_t, 128, 128, 256>(),
-      V<uint32_t, 64, 64, 256>(),  V<uint32_t, 32, 256, 256>(), V<uint32_t, 64, 256, 256>(),
-      V<uint32_t, 32, 128, 256>(), V<uint32_t, 64, 128, 256>(),
-      V<uint64_t, 64, 64, 256>(),  V<uint64_t, 16, 128, 256>(), V<uint64_t, 32, 128, 256>(),
-      V<uint64_t, 16, 256, 256>(), V<uint64_t, 32, 64, 256>(),  V<uint64_t, 32, 256, 256>(),
+      V<uint32_t, 64, 256, 256>(),  V<uint32_t, 64, 256, 512>(),  V<uint32_t, 128, 256, 1024>(),
+      V<uint32_t, 128, 128, 512>(), V<uint32_t, 256, 128, 1024>(), V<uint32_t, 64, 512, 1024>(),
+      V<uint32_t, 128, 128, 256>(), V<uint32_t, 32, 256, 256>(),
+      V<uint64_t, 32, 256, 256>(),  V<uint64_t, 64, 128, 512>(),  V<uint64_t, 64, 256, 1024>(),
+      V<uint16_t, 128, 256, 256>(), V<uint16_t, 128, 256, 512>(), V<uint16_t, 256, 256, 1024>(),
   };
   int cur_es = 0;
   for (auto& v : vs) {
