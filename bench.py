@@ -38,11 +38,13 @@ CONFIGS = {
     "C2": ((2000, 512, 512), np.float32, 1,
            "C2: float32 (2000,512,512) per GPU, key=time; swap((0,),(0,1)) + mean/std over time"),
     "C3": ((4096, 256, 256, 32), np.float32, 2,
-           "C3: float32 (4096,256,256,32) per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
+           "C3: float32 (4096,256,256,32) per GPU, keys (0,1); swap((0,),(0,)) + .T"),
     "C4": ((10000, 1024, 1024), np.uint16, 1,
-           "C4: uint16 (10000,1024,1024) per GPU, key 0; swap((0,),(0,)) + var over axis 0"),
+           "C4: uint16 (10000,1024,1024) per GPU, key 0; swap((0,),(0,)) + chunk('150') -> unchunk "
+           "+ float64 var over axis 0"),
     "C5": ((64, 64, 64, 64, 64), np.float64, 3,
-           "C5: float64 64^5 per GPU, keys (0,1,2); .T + mean/std over axis 0"),
+           "C5: float64 64^5 per GPU, keys (0,1,2); .T + transpose(2,0,4,1,3) + "
+           "chunk((16,16), padding=2) -> unchunk"),
     "target64": ((8192, 256, 256, 32), np.float32, 2,
                  "64 GiB float32 4-D per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
 }
@@ -61,7 +63,11 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(cfg, kernel_substr="k_transpose"):
+ROOFLINE_KERNEL = {"C2": "k_transpose", "C5": "k_transpose", "C3": "k_rowcopy", "C4": "k_rowcopy",
+                   "target64": "k_rowcopy"}
+
+
+def pmc_traffic(cfg, kernel_substr=None):
     """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters.
 
     Two separate child runs of this script (swap only), one counter each
@@ -76,6 +82,7 @@ def pmc_traffic(cfg, kernel_substr="k_transpose"):
     import shutil
     import subprocess
     import tempfile
+    kernel_substr = kernel_substr or ROOFLINE_KERNEL[cfg]
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None, "rocprofv3 not found"
@@ -119,37 +126,47 @@ def synth_shard(torch, shape, dtype, device, seed):
     raise ValueError(dtype)
 
 
-def workload(cfg, b):
-    """The step for a config: returns (swapped, [stat results])."""
+def steps_of(cfg, b, world=1):
+    """The step of a config as (name, call, algorithmic bytes of all ranks) in order.
+
+    The first op is the swap / transpose whose kernel is the roofline line.
+    Bytes: permute 2*N*s; statistic N*s + outputs; chunk pack
+    N*s + packed bytes, unchunk packed bytes + N*s.
+    """
+    n = int(np.prod(b.shape)) // world   # elements per rank (weak scaling: equal slabs)
+    s = b.dtype.itemsize
+    N = n * s
     if cfg == "C2":
-        s = b.swap((0,), (0, 1))
-        return s, [s.mean(axis=2), s.std(axis=2)]
-    if cfg in ("C3", "target64"):
-        s = b.swap((0,), (0,))
-        return s, [b.mean(axis=0), b.std(axis=0)]
+        out = b.shape[1] * b.shape[2] * 4 // world
+        sw = {}
+        return [("swap", lambda: sw.__setitem__("s", b.swap((0,), (0, 1))), 2 * N),
+                ("mean", lambda: sw["s"].mean(axis=2), N + out),
+                ("std", lambda: sw["s"].std(axis=2), N + out)]
+    if cfg == "target64":
+        out = (n * world // b.shape[0]) * s
+        return [("swap", lambda: b.swap((0,), (0,)), 2 * N),
+                ("mean", lambda: b.mean(axis=0), N + out),
+                ("std", lambda: b.std(axis=0), N + out)]
+    if cfg == "C3":
+        return [("swap", lambda: b.swap((0,), (0,)), 2 * N),
+                ("T", lambda: b.T, 2 * N)]
     if cfg == "C4":
-        s = b.swap((0,), (0,))
-        return s, [b.var(axis=0)]
+        from bolt_amd.mi355x.plan import ChunkGeometry, getplan
+        plan, pad = getplan(b.shape[1:], b.dtype, "150")
+        P = ChunkGeometry(b.shape[1:], plan, pad).size * (b.shape[0] // world) * s
+        ck = {}
+        return [("swap", lambda: b.swap((0,), (0,)), 2 * N),
+                ("chunk", lambda: ck.__setitem__("c", b.chunk("150")), N + P),
+                ("unchunk", lambda: ck.pop("c").unchunk(), P + N),
+                ("var", lambda: b.var(axis=0), N + (n * world // b.shape[0]) * 8)]
     if cfg == "C5":
-        s = b.T
-        return s, [b.mean(axis=0), b.std(axis=0)]
-    raise ValueError(cfg)
-
-
-def step_bytes(cfg, global_shape, dtype):
-    n = int(np.prod(global_shape))
-    s = np.dtype(dtype).itemsize
-    if cfg == "C2":
-        out = global_shape[1] * global_shape[2]
-        ob = np.dtype(np.float32).itemsize
-        return {"swap": 2 * n * s, "mean": n * s + out * ob, "std": n * s + out * ob}
-    if cfg in ("C3", "target64", "C5"):
-        out = n // global_shape[0]
-        ob = s
-        return {"swap": 2 * n * s, "mean": n * s + out * ob, "std": n * s + out * ob}
-    if cfg == "C4":
-        out = n // global_shape[0]
-        return {"swap": 2 * n * s, "var": n * s + out * 8}
+        from bolt_amd.mi355x.plan import ChunkGeometry
+        P = ChunkGeometry(b.shape[3:], (16, 16), (2, 2)).size * (n // int(np.prod(b.shape[3:]))) * s
+        ck = {}
+        return [("T", lambda: b.T, 2 * N),
+                ("transpose", lambda: b.transpose(2, 0, 4, 1, 3), 2 * N),
+                ("chunk", lambda: ck.__setitem__("c", b.chunk((16, 16), padding=2)), N + P),
+                ("unchunk", lambda: ck.pop("c").unchunk(), P + N)]
     raise ValueError(cfg)
 
 
@@ -169,8 +186,9 @@ def cpu_baseline(cfg, shape, dtype, rows):
     t2 = time.perf_counter()
     O.stat(s, 'stdev', axis=2)
     t3 = time.perf_counter()
-    b = step_bytes(cfg, sample_shape, dtype)
-    total = sum(b.values())
+    N = int(np.prod(sample_shape)) * np.dtype(dtype).itemsize
+    out = sample_shape[1] * sample_shape[2] * 4
+    total = 2 * N + 2 * (N + out)
     return {"value": total / (t3 - t0) / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s: "
                       "swap((0,),(0,1)) %.2fs + mean(axis=2) %.2fs + std(axis=2) %.2fs"
@@ -207,17 +225,18 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    if args.pmc_child:  # profiled child of pmc_traffic(): swaps only, no output
+    ops = steps_of(args.config, b, world)
+    if args.pmc_child:  # profiled child of pmc_traffic(): the roofline op only, no output
         for _ in range(args.warmup + args.steps):
-            s, _ = (b.swap((0,), (0, 1)) if args.config == "C2" else
-                    b.T if args.config == "C5" else b.swap((0,), (0,))), None
-            del s
+            r = ops[0][1]()
+            del r
         torch.cuda.synchronize()
         return
 
     for _ in range(args.warmup):
-        s, stats = workload(args.config, b)
-        del s, stats
+        for _, call, _ in ops:
+            r = call()
+            del r
     barrier()
 
     stream = torch.cuda.current_stream(dev)
@@ -228,8 +247,11 @@ def main():
     be = backend_for(dev)
     kev = []
     permute0 = be.permute
+    timing = {"on": False}
 
     def timed_permute(*a, **k):
+        if not timing["on"]:
+            return permute0(*a, **k)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(torch.cuda.current_stream(dev))
         permute0(*a, **k)
@@ -242,28 +264,15 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        s = workload_swap = None
-        if args.config == "C2":
-            s = b.swap((0,), (0, 1))
-            ev[i][1].record(stream)
-            s.mean(axis=2)
-            s.std(axis=2)
-        elif args.config in ("C3", "target64"):
-            s = b.swap((0,), (0,))
-            ev[i][1].record(stream)
-            b.mean(axis=0)
-            b.std(axis=0)
-        elif args.config == "C4":
-            s = b.swap((0,), (0,))
-            ev[i][1].record(stream)
-            b.var(axis=0)
-        else:
-            s = b.T
-            ev[i][1].record(stream)
-            b.mean(axis=0)
-            b.std(axis=0)
-        del s, workload_swap
+        for k, (_, call, _) in enumerate(ops):
+            if k == 0:
+                ev[i][0].record(stream)
+                timing["on"] = True
+            r = call()
+            if k == 0:
+                timing["on"] = False
+                ev[i][1].record(stream)
+            del r
     barrier()
     elapsed = time.perf_counter() - t0
     be.permute = permute0
@@ -279,10 +288,10 @@ def main():
 
     swap_ms = float(np.mean([a.elapsed_time(z) for a, z in ev]))   # the whole swap call
     kern_ms = float(np.mean([a.elapsed_time(z) for a, z in kev])) if kev else swap_ms
-    per = step_bytes(args.config, gshape, dtype)
+    per = {name: nb * world for name, _, nb in ops}
     total = sum(per.values()) * args.steps
     value = total / elapsed / 1e9
-    swap_bytes_rank = per["swap"] / world
+    swap_bytes_rank = ops[0][2]
     achieved = swap_bytes_rank / (kern_ms / 1e3) / 1e9
 
     line = {
@@ -303,7 +312,7 @@ def main():
                    "bytes_per_step": {k: int(v) for k, v in per.items()}},
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_transpose (bm_permute) for the swap" if world == 1 else
+            "kernel": "%s (bm_permute) for the %s" % (ROOFLINE_KERNEL[args.config], ops[0][0]) if world == 1 else
                       "swap = pack + RCCL all_to_all + unpack (per rank)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
@@ -317,7 +326,7 @@ def main():
     }
     if world > 1:
         G = world
-        n_rank = per["swap"] / 2 / G                  # bytes held per rank
+        n_rank = ops[0][2] / 2                        # bytes held per rank
         payload = n_rank * (G - 1) / G                # bytes each rank sends to its peers
         ex = phases.get("exchange")
         if ex:  # the swap across GPUs: pipelined pack -> RCCL all-to-all -> unpack
