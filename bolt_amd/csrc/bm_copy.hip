@@ -37,6 +37,17 @@ constexpr int kThreads = 256;
 #define BM_RC_GRIDCAP 16777208  // one vector per lane, a block per 256 vectors, up to the 2^32-thread launch limit
                                 // (profiles/r01_ab3..ab5: many blocks +15-25% on C3/C4 swaps)
 #endif
+#ifndef BM_PK
+#define BM_PK 1  // packed-word tiles for 1-/2-byte transposes (A/B knob)
+#endif
+#ifndef BM_PK16_TA  // packed tiles, profiles/r01_ab_pk2.log: u16 128x256 +9%, u8 128x256 +11% over
+#define BM_PK16_TA 128  // element-wise LDS tiles (64x512 / 128x512 / 256x256 measured and lose)
+#define BM_PK16_TB 256
+#endif
+#ifndef BM_PK8_TA
+#define BM_PK8_TA 128
+#define BM_PK8_TB 256
+#endif
 #ifndef BM_RC_XCD
 #define BM_RC_XCD 0  // XCD-grouped covering grid: +5% in a C4 microbench (r01_rc1) but -3..-20% in the product A/B (r01_ab_rc)
 #endif
@@ -190,6 +201,102 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+
+// ------------------------------------------------------ packed transpose --
+// 1- and 2-byte elements: P = 4 / sizeof(T) consecutive source rows (along b)
+// are packed into 32-bit words, one word per column a, so the LDS tile is a
+// 32-bit transpose of TA x (TB / P) words -- no 8-/16-bit LDS traffic.  A
+// lane loads P 16-B rows, writes VA words; the store side reads 4 words along
+// b (4 * P consecutive elements = 16 B) and stores them as one vector.
+// Requires 16-B aligned source and destination rows (the caller checks).
+// (tile sweep: element-wise LDS tiles move u16 / u8 at 4.6 / 3.0 TB/s,
+// profiles/r01_tt2.log)
+template <typename T, int TA, int TB>
+__global__ void __launch_bounds__(kThreads)
+    k_transpose_pk(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
+  constexpr int P = 4 / (int)sizeof(T);  // rows per word
+  constexpr int VA = 16 / (int)sizeof(T);
+  constexpr int TBW = TB / P;            // word rows in the tile
+  constexpr int NVA = TA / VA;           // lanes per word row (load)
+  constexpr int RGA = kThreads / NVA;    // word rows per pass
+  constexpr int NL = TBW / RGA;
+  constexpr int NVB = TBW / 4;           // lanes per destination row (4 words each)
+  constexpr int RPB = kThreads / NVB;
+  constexpr int NS = TA / RPB;
+  constexpr int BITS = 8 * (int)sizeof(T);
+  static_assert(NL >= 1 && TBW % RGA == 0 && NS >= 1 && TA % RPB == 0, "tile too small for the thread layout");
+  static_assert(NL * P * 4 <= 64, "loads in flight exceed the register budget");
+  __shared__ uint32_t tile[TBW][TA + 1];
+  const int tx = threadIdx.x % NVA, ty = threadIdx.x / NVA;
+  const int ux = threadIdx.x % NVB, uy = threadIdx.x / NVB;
+  const int ia = tx * VA;
+
+  for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
+    const uint64_t bt = fd_div(t, d.ntAB);
+    const uint64_t rem = t - bt * d.ntAB.d;
+    const uint64_t ta = fd_div(rem, d.ntB);
+    const uint64_t tb = rem - ta * d.ntB.d;
+    int64_t so, dof;
+    decomp2(bt, d.batch, so, dof);
+    const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
+
+    const T *s = src + so + a0 + b0 * d.sb;
+    const bool fullA = (a0 + ia + VA <= d.La);
+    T v[NL][P][VA];
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int wr = ty + it * RGA;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int rb = wr * P + j;
+        const T *p = s + ia + (int64_t)rb * d.sb;
+        if (b0 + rb < d.Lb && fullA) {
+          vload_nt<T, VA>(p, v[it][j]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < VA; ++k) v[it][j][k] = (b0 + rb < d.Lb && a0 + ia + k < d.La) ? p[k] : T(0);
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int wr = ty + it * RGA;
+#pragma unroll
+      for (int k = 0; k < VA; ++k) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) w |= (uint32_t)v[it][j][k] << (j * BITS);
+        tile[wr][ia + k] = w;
+      }
+    }
+    __syncthreads();
+
+    T *q = dst + dof + b0 + a0 * d.da;
+    const int ib = ux * 4 * P;  // first element of this lane's 16 B along b
+    const bool fullB = (b0 + ib + 4 * P <= d.Lb);
+#pragma unroll
+    for (int it = 0; it < NS; ++it) {
+      const int ra = uy + it * RPB;
+      if (a0 + ra < d.La) {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = tile[ux * 4 + k][ra];
+        T *p = q + (int64_t)ra * d.da + ib;
+        if (fullB) {
+          typedef typename VecB<16>::t V16;
+          V16 x;
+          __builtin_memcpy(&x, w, 16);
+          __builtin_nontemporal_store(x, reinterpret_cast<V16 *>(p));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4 * P; ++e)
+            if (b0 + ib + e < d.Lb) p[e] = (T)(w[e / P] >> ((e % P) * BITS));
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
 
 // ------------------------------------------------------------ runs transpose --
 // A permutation that keeps a short innermost run (W 16-B units, 32-256 B) but
@@ -458,6 +565,24 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   for (int k = 0; k < (int)dims.size(); ++k) {
     if (k != a && (dims[k].ss * es) % 16) va = false;
     if (k != b && (dims[k].ds * es) % 16) vb = false;
+  }
+  if (BM_PK && va && vb && (es == 1 || es == 2)) {
+    // packed-word tiles: 128-B source and 1-KiB destination segments
+    const int ta = es == 2 ? BM_PK16_TA : BM_PK8_TA, tbb = es == 2 ? BM_PK16_TB : BM_PK8_TB;
+    TransDesc tp = td;
+    const uint64_t pA = (uint64_t)((td.La + ta - 1) / ta), pB = (uint64_t)((td.Lb + tbb - 1) / tbb);
+    tp.ntB = make_fastdiv(pB);
+    tp.ntAB = make_fastdiv(pA * pB);
+    tp.ntiles = pA * pB * nb;
+    uint64_t g = tp.ntiles;
+    if (g > kMaxGrid) g = kMaxGrid;
+    if (es == 2)
+      k_transpose_pk<uint16_t, BM_PK16_TA, BM_PK16_TB><<<(int)g, kThreads, 0, st>>>((const uint16_t *)src,
+                                                                                 (uint16_t *)dst, tp);
+    else
+      k_transpose_pk<uint8_t, BM_PK8_TA, BM_PK8_TB><<<(int)g, kThreads, 0, st>>>((const uint8_t *)src,
+                                                                              (uint8_t *)dst, tp);
+    return BM_OK;
   }
   switch (es) {
     case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, st);

@@ -75,6 +75,11 @@ def test_permute_all_perms_4d(dtype):
     ((6, 40, 30, 16), (0, 2, 1, 3)),
     ((40, 7, 30, 16), (2, 1, 0, 3)),
     ((130, 3, 129, 32), (2, 1, 0, 3)),
+    # 1-/2-byte transposes on 16-B aligned rows: packed-word tiles, ragged edges
+    ((1000, 40), (1, 0)),
+    ((528, 2, 144), (2, 1, 0)),
+    ((1040, 3, 96), (2, 1, 0)),
+    ((48, 1600), (1, 0)),
 ])
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64, np.complex128])
 def test_permute_shapes(shape, perm, dtype):

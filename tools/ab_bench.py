@@ -107,6 +107,9 @@ OPS = {
     "c3_full": lambda: Permute((4096, 256, 256, 32), (1, 2, 0, 3), np.float32),
     "t64_swap": lambda: Permute((8192, 256, 256, 32), (1, 2, 0, 3), np.float32),
     "c4_full": lambda: Permute((10000, 1024, 1024), (1, 0, 2), np.uint16),
+    "u16_T": lambda: Permute((2000, 1024, 1024), (2, 1, 0), np.uint16),
+    "u8_T": lambda: Permute((2000, 1024, 2048), (2, 1, 0), np.uint8),
+    "u16_2d": lambda: Permute((2000, 1048576), (1, 0), np.uint16),
     "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
     "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
     "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),
