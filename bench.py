@@ -189,11 +189,23 @@ def cpu_baseline(cfg, shape, dtype, rows):
     N = int(np.prod(sample_shape)) * np.dtype(dtype).itemsize
     out = sample_shape[1] * sample_shape[2] * 4
     total = 2 * N + 2 * (N + out)
+    # the reference's local mode (bolt/local/array.py) runs the same three calls
+    # as numpy on one host thread: ascontiguousarray(transpose) + mean / std
+    u0 = time.perf_counter()
+    xs = np.ascontiguousarray(x.transpose(1, 2, 0))
+    u1 = time.perf_counter()
+    xs.mean(axis=2)
+    u2 = time.perf_counter()
+    xs.std(axis=2)
+    u3 = time.perf_counter()
     return {"value": total / (t3 - t0) / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s: "
                       "swap((0,),(0,1)) %.2fs + mean(axis=2) %.2fs + std(axis=2) %.2fs"
                       % (str(sample_shape), t1 - t0, t2 - t1, t3 - t2),
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(),
+            "local_numpy": {"value": round(total / (u3 - u0) / 1e9, 3), "unit": "GB/s", "cores": 1,
+                            "sample": "the reference local mode's numpy calls on the same input: transpose "
+                                      "%.2fs + mean %.2fs + std %.2fs" % (u1 - u0, u2 - u1, u3 - u2)}}
 
 
 def main():

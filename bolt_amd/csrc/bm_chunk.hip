@@ -17,21 +17,36 @@
 // element out of LDS through the map (int32, L2-resident, shared by all
 // records).  HBM traffic = the algorithmic bytes: src_rec + dst_rec element
 // bytes per record, each byte moved once; the halo re-reads come from LDS.
+//
+// Parts: the host may split a record's destination into up to 8 ranges
+// [dlo, dhi), each reading only the source range [slo, shi) it needs (chunks
+// are laid out band by band, so these ranges are short); a tile is then one
+// (record, part) and stages (shi - slo) elements -- a smaller LDS footprint,
+// more blocks per CU.
 // Larger records use the direct form (map lookups straight from HBM/L2).
 #include "bm_common.h"
 #include "../../include/bolt_mi355x.h"
+
+#include <algorithm>
 
 namespace {
 
 constexpr int kCThreads = 256;
 constexpr int64_t kStageBytes = 32768;   // LDS per tile when records are small (5 blocks / CU)
 constexpr int64_t kMaxStageBytes = 65536;
+constexpr int kMaxParts = 8;
 
 template <int ES> struct Elem;
 template <> struct Elem<1> { typedef uint8_t t; };
 template <> struct Elem<2> { typedef uint16_t t; };
 template <> struct Elem<4> { typedef uint32_t t; };
 template <> struct Elem<8> { typedef uint64_t t; };
+
+struct Parts {
+  int32_t n;
+  int32_t pad_;
+  int64_t dlo[kMaxParts], dhi[kMaxParts], slo[kMaxParts], shi[kMaxParts];
+};
 
 // LB: staging load width in bytes (16 when the tile's bytes are 16-B aligned)
 template <int ES, int VEC, int LB>
@@ -72,6 +87,41 @@ __global__ void __launch_bounds__(kCThreads)
   }
 }
 
+// one (record, part) per tile: stage src[slo, shi) of the record, write dst[dlo, dhi)
+template <int ES, int VEC, int LB>
+__global__ void __launch_bounds__(kCThreads)
+    k_recmap_parts(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ map,
+                   Parts P, int64_t src_rec, int64_t dst_rec, int64_t nrec) {
+  typedef typename Elem<ES>::t T;
+  typedef typename VecB<LB>::t L;
+  typedef typename VecB<ES * VEC>::t V;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const T *lds = reinterpret_cast<const T *>(smem);
+  const int64_t ntiles = nrec * P.n;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t r = t / P.n;
+    const int p = (int)(t - r * P.n);
+    const int64_t slo = P.slo[p], dlo = P.dlo[p];
+    const int64_t nld = (P.shi[p] - slo) * ES / LB;
+    const L *s = reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES);
+    L *sl = reinterpret_cast<L *>(smem);
+    for (int64_t i = threadIdx.x; i < nld; i += kCThreads) sl[i] = __builtin_nontemporal_load(s + i);
+    __syncthreads();
+    const int64_t nout = (P.dhi[p] - dlo) / VEC;
+    V *d = reinterpret_cast<V *>(dst + (r * dst_rec + dlo) * ES);
+    for (int64_t i = threadIdx.x; i < nout; i += kCThreads) {
+      const int64_t o = dlo + i * VEC;
+      T v[VEC];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) v[k] = lds[map[o + k] - slo];
+      V w;
+      __builtin_memcpy(&w, v, sizeof(V));
+      __builtin_nontemporal_store(w, d + i);
+    }
+    __syncthreads();
+  }
+}
+
 template <int ES>
 __global__ void __launch_bounds__(kCThreads)
     k_recmap_direct(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ map,
@@ -87,30 +137,46 @@ __global__ void __launch_bounds__(kCThreads)
   }
 }
 
+struct Launch {
+  const char *src;
+  char *dst;
+  const int32_t *map;
+  int64_t src_rec, dst_rec, nrec, rb;
+  const Parts *parts;  // null: whole records, rb per tile
+  int grid;
+  size_t shmem;
+  hipStream_t st;
+};
+
+template <int ES, int VEC, int LB>
+void launch_one(const Launch &L) {
+  if (L.parts)
+    k_recmap_parts<ES, VEC, LB><<<L.grid, kCThreads, L.shmem, L.st>>>(L.src, L.dst, L.map, *L.parts, L.src_rec,
+                                                                       L.dst_rec, L.nrec);
+  else
+    k_recmap_lds<ES, VEC, LB><<<L.grid, kCThreads, L.shmem, L.st>>>(L.src, L.dst, L.map, L.src_rec, L.dst_rec,
+                                                                     L.nrec, L.rb, make_fastdiv((uint64_t)L.dst_rec));
+}
+
 template <int ES, int VEC>
-void launch_lds_v(const char *src, char *dst, const int32_t *map, int64_t src_rec, int64_t dst_rec,
-                  int64_t nrec, int64_t rb, int lb, int grid, size_t shmem, hipStream_t st) {
-  const FastDiv f = make_fastdiv((uint64_t)dst_rec);
+void launch_lb(const Launch &L, int lb) {
   switch (lb) {
-    case 16: k_recmap_lds<ES, VEC, 16><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
-    case 8: k_recmap_lds<ES, VEC, 8><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
-    case 4: k_recmap_lds<ES, VEC, 4><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
-    case 2: k_recmap_lds<ES, VEC, 2><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
-    default: k_recmap_lds<ES, VEC, 1><<<grid, kCThreads, shmem, st>>>(src, dst, map, src_rec, dst_rec, nrec, rb, f); break;
+    case 16: launch_one<ES, VEC, 16>(L); break;
+    case 8: launch_one<ES, VEC, 8>(L); break;
+    case 4: launch_one<ES, VEC, 4>(L); break;
+    case 2: launch_one<ES, VEC, 2>(L); break;
+    default: launch_one<ES, VEC, 1>(L); break;
   }
 }
 
 template <int ES>
-void launch_lds(const char *src, char *dst, const int32_t *map, int64_t src_rec, int64_t dst_rec,
-                int64_t nrec, int64_t rb, int lb, int vec, int grid, size_t shmem, hipStream_t st) {
+void launch_lds(const Launch &L, int lb, int vec) {
   constexpr int V16 = 16 / ES;
-  if (vec >= V16) return launch_lds_v<ES, V16>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
-  if (ES <= 4 && vec >= 8 / ES)
-    return launch_lds_v<ES, (8 / ES > 0 ? 8 / ES : 1)>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
-  if (ES <= 2 && vec >= 4 / ES)
-    return launch_lds_v<ES, (4 / ES > 0 ? 4 / ES : 1)>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
-  if (ES == 1 && vec >= 2) return launch_lds_v<ES, 2>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
-  launch_lds_v<ES, 1>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, grid, shmem, st);
+  if (vec >= V16) return launch_lb<ES, V16>(L, lb);
+  if (ES <= 4 && vec >= 8 / ES) return launch_lb<ES, (8 / ES > 0 ? 8 / ES : 1)>(L, lb);
+  if (ES <= 2 && vec >= 4 / ES) return launch_lb<ES, (4 / ES > 0 ? 4 / ES : 1)>(L, lb);
+  if (ES == 1 && vec >= 2) return launch_lb<ES, 2>(L, lb);
+  launch_lb<ES, 1>(L, lb);
 }
 
 int pow2_align(uintptr_t a, int64_t bytes, int cap) {
@@ -122,12 +188,38 @@ int pow2_align(uintptr_t a, int64_t bytes, int cap) {
 }  // namespace
 
 extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int64_t src_rec, int64_t dst_rec,
-                                const int32_t *map, int elem_bytes, void *stream) {
-  if (nrec < 0 || src_rec <= 0 || dst_rec <= 0 || src_rec > 0x7fffffffLL ||
-      (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8)) {
-    bm_set_error("bm_record_gather: bad arguments (nrec %lld, src_rec %lld, dst_rec %lld, elem_bytes %d)",
-                 (long long)nrec, (long long)src_rec, (long long)dst_rec, elem_bytes);
+                                const int32_t *map, int nparts, const int64_t *parts, int elem_bytes,
+                                void *stream) {
+  if (nrec < 0 || src_rec <= 0 || dst_rec <= 0 || src_rec > 0x7fffffffLL || nparts < 0 || nparts > kMaxParts ||
+      (nparts > 1 && !parts) || (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8)) {
+    bm_set_error("bm_record_gather: bad arguments (nrec %lld, src_rec %lld, dst_rec %lld, nparts %d, elem_bytes %d)",
+                 (long long)nrec, (long long)src_rec, (long long)dst_rec, nparts, elem_bytes);
     return BM_E_ARG;
+  }
+  const int es = elem_bytes;
+  Parts P;
+  P.n = nparts > 1 ? nparts : 1;
+  P.pad_ = 0;
+  int64_t span = src_rec;
+  if (nparts > 1) {  // the ranges must tile [0, dst_rec) in order, sources inside the record
+    int64_t at = 0;
+    span = 0;
+    for (int p = 0; p < nparts; ++p) {
+      const int64_t dlo = parts[4 * p], dhi = parts[4 * p + 1], slo = parts[4 * p + 2], shi = parts[4 * p + 3];
+      if (dlo != at || dhi <= dlo || slo < 0 || shi <= slo || shi > src_rec) {
+        bm_set_error("bm_record_gather: part %d [%lld, %lld) <- [%lld, %lld) does not tile the record", p,
+                     (long long)dlo, (long long)dhi, (long long)slo, (long long)shi);
+        return BM_E_ARG;
+      }
+      P.dlo[p] = dlo; P.dhi[p] = dhi; P.slo[p] = slo; P.shi[p] = shi;
+      span = std::max(span, shi - slo);
+      at = dhi;
+    }
+    if (at != dst_rec || span * es > kMaxStageBytes) {
+      bm_set_error("bm_record_gather: parts cover %lld of %lld elements, widest source range %lld B",
+                   (long long)at, (long long)dst_rec, (long long)(span * es));
+      return BM_E_ARG;
+    }
   }
   if (nrec == 0) return BM_OK;
   if (!src_ || !dst_ || !map) {
@@ -137,21 +229,38 @@ extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int6
   const char *src = static_cast<const char *>(src_);
   char *dst = static_cast<char *>(dst_);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int es = elem_bytes;
   const int64_t rec_bytes = src_rec * es;
-  if (rec_bytes <= kMaxStageBytes) {
-    int64_t rb = rec_bytes >= kStageBytes ? 1 : kStageBytes / rec_bytes;
-    if (rb > nrec) rb = nrec;
-    const int64_t ntiles = (nrec + rb - 1) / rb;
-    const size_t shmem = (size_t)(rb * rec_bytes + 15) / 16 * 16;
-    const int lb = pow2_align((uintptr_t)src, rec_bytes, 16);          // every tile start aligned
-    const int vec = pow2_align((uintptr_t)dst, dst_rec * es, 16) / es;  // elements per store
-    const int grid = (int)(ntiles < 16384 ? ntiles : 16384);
+  if (span * es <= kMaxStageBytes) {
+    Launch L;
+    L.src = src; L.dst = dst; L.map = map;
+    L.src_rec = src_rec; L.dst_rec = dst_rec; L.nrec = nrec; L.st = st;
+    int lb = pow2_align((uintptr_t)src, rec_bytes, 16);     // every tile start aligned
+    int vb = pow2_align((uintptr_t)dst, dst_rec * es, 16);  // bytes per store
+    int64_t ntiles;
+    if (nparts > 1) {
+      for (int p = 0; p < nparts; ++p) {
+        lb = std::min(lb, pow2_align((uintptr_t)(P.slo[p] * es), (P.shi[p] - P.slo[p]) * es, 16));
+        vb = std::min(vb, pow2_align((uintptr_t)(P.dlo[p] * es), (P.dhi[p] - P.dlo[p]) * es, 16));
+      }
+      L.rb = 1;
+      L.parts = &P;
+      L.shmem = (size_t)(span * es + 15) / 16 * 16;
+      ntiles = nrec * nparts;
+    } else {
+      int64_t rb = rec_bytes >= kStageBytes ? 1 : kStageBytes / rec_bytes;
+      if (rb > nrec) rb = nrec;
+      L.rb = rb;
+      L.parts = nullptr;
+      L.shmem = (size_t)(rb * rec_bytes + 15) / 16 * 16;
+      ntiles = (nrec + rb - 1) / rb;
+    }
+    L.grid = (int)(ntiles < 16384 ? ntiles : 16384);
+    const int vec = std::max(1, vb / es);
     switch (es) {
-      case 1: launch_lds<1>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
-      case 2: launch_lds<2>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
-      case 4: launch_lds<4>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
-      default: launch_lds<8>(src, dst, map, src_rec, dst_rec, nrec, rb, lb, vec, grid, shmem, st); break;
+      case 1: launch_lds<1>(L, lb, vec); break;
+      case 2: launch_lds<2>(L, lb, vec); break;
+      case 4: launch_lds<4>(L, lb, vec); break;
+      default: launch_lds<8>(L, lb, vec); break;
     }
   } else {
     const uint64_t total = (uint64_t)nrec * (uint64_t)dst_rec;

@@ -42,6 +42,37 @@ def dtype_code(dtype):
         raise NotImplementedError("statistics over dtype %s are not supported by the mi355x mode" % dt)
 
 
+PART_BYTES = 24576  # LDS per (record, part) tile of bm_record_gather: 6 blocks per CU
+
+
+def record_parts(rmap, src_rec, es, part_bytes=None):
+    """Split a record map into <= 8 destination ranges whose source ranges fit
+    ``part_bytes`` of LDS, as a flat [dlo, dhi, slo, shi, ...] list ([] = one
+    whole-record tile).  Ranges are 16-B aligned; the split is taken only if
+    the staged bytes stay within 1.25x of the record (halo rows re-read)."""
+    import os
+    part_bytes = PART_BYTES if part_bytes is None else part_bytes
+    if os.environ.get("BOLT_AMD_RECMAP_PARTS", "1") == "0" or src_rec * es <= part_bytes:
+        return []
+    al = max(1, 16 // es)
+    n = rmap.size
+    for k in range(2, 9):
+        cut = [(n * i // k) // al * al for i in range(k)] + [n]
+        if any(b <= a for a, b in zip(cut[:-1], cut[1:])):
+            break
+        out, staged, widest = [], 0, 0
+        for a, b in zip(cut[:-1], cut[1:]):
+            seg = rmap[a:b]
+            slo = int(seg.min()) // al * al
+            shi = min(src_rec, -(-(int(seg.max()) + 1) // al) * al)
+            out += [a, b, slo, shi]
+            staged += shi - slo
+            widest = max(widest, shi - slo)
+        if widest * es <= part_bytes and staged <= 1.25 * src_rec:
+            return out
+    return []
+
+
 class HipBackend(object):
     """Launches libbolt_mi355x kernels on torch's current stream."""
 
@@ -106,16 +137,19 @@ class HipBackend(object):
         """
         import torch
         ck = (src.device, key)
-        dmap = self._maps.get(ck)
-        if dmap is None:
+        hit = self._maps.get(ck)
+        if hit is None:
             rmap = np.ascontiguousarray(rmap, dtype=np.int32)
             if rmap.size != dst_rec or rmap.min() < 0 or rmap.max() >= src_rec:
                 raise ValueError("record map does not match the record sizes")
-            dmap = torch.from_numpy(rmap).to(src.device)
-            self._maps[ck] = dmap
+            parts = record_parts(rmap, int(src_rec), int(es))
+            hit = (torch.from_numpy(rmap).to(src.device), len(parts) // 4,
+                   _lib.i64_array(parts) if parts else None)
+            self._maps[ck] = hit
+        dmap, nparts, parts = hit
         _lib.check(self.lib.bm_record_gather(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
                                              int(src_rec), int(dst_rec), ctypes.c_void_p(dmap.data_ptr()),
-                                             int(es), self._stream(src)), "bm_record_gather")
+                                             nparts, parts, int(es), self._stream(src)), "bm_record_gather")
 
     def _workspace(self, stat, code, O, R, I, device):
         import torch

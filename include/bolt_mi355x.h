@@ -127,9 +127,15 @@ int bm_gather_rows(const void *src, void *dst, int64_t n_outer, int64_t src_rows
  *   unpack ChunkedArray.unchunk/removepad  bolt/spark/chunk.py:146-200, :514-550
  *          (map: dense value index -> packed element of its chunk's core)
  * A source record of <= 64 KiB is staged whole in LDS; bit-exact.
+ * parts (HOST array, nparts <= 8; nparts 0 or 1 = the whole record): the
+ * destination record split into ranges, part p = {dlo, dhi, slo, shi}:
+ * dst[dlo, dhi) reads only src[slo, shi) (every map entry of the range lies
+ * there; the caller guarantees it), staged alone -- a smaller LDS tile.  The
+ * ranges must tile [0, dst_rec) in order.
  */
 int bm_record_gather(const void *src, void *dst, int64_t nrec, int64_t src_rec,
-                     int64_t dst_rec, const int32_t *map, int elem_bytes, void *stream);
+                     int64_t dst_rec, const int32_t *map, int nparts,
+                     const int64_t *parts, int elem_bytes, void *stream);
 
 /*
  * Reductions over a C-contiguous array viewed as [O][R][I]: the middle axis

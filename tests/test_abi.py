@@ -55,11 +55,18 @@ def test_argument_errors(lib):
     assert lib.bm_gather_rows(None, None, 1, 4, 8, None, 3, None) == -1
     assert b"null pointer" in lib.bm_last_error()
     assert lib.bm_gather_rows(None, None, 0, 4, 8, None, 3, None) == 0  # nothing to move
-    assert lib.bm_record_gather(None, None, 4, 8, 8, None, 16, None) == -1
+    assert lib.bm_record_gather(None, None, 4, 8, 8, None, 0, None, 16, None) == -1
     assert b"bad arguments" in lib.bm_last_error()
-    assert lib.bm_record_gather(None, None, 4, 8, 8, None, 8, None) == -1
+    assert lib.bm_record_gather(None, None, 4, 8, 8, None, 0, None, 8, None) == -1
     assert b"null pointer" in lib.bm_last_error()
-    assert lib.bm_record_gather(None, None, 0, 8, 8, None, 8, None) == 0  # nothing to move
+    assert lib.bm_record_gather(None, None, 0, 8, 8, None, 0, None, 8, None) == 0  # nothing to move
+    # parts must tile the destination record in order, sources inside the record
+    assert lib.bm_record_gather(None, None, 1, 8, 8, None, 2, _lib.i64_array([0, 4, 0, 4, 5, 8, 4, 8]), 8,
+                                None) == -1
+    assert b"does not tile" in lib.bm_last_error()
+    assert lib.bm_record_gather(None, None, 1, 8, 8, None, 2, _lib.i64_array([0, 4, 0, 4, 4, 8, 4, 9]), 8,
+                                None) == -1
+    assert lib.bm_record_gather(None, None, 1, 8, 8, None, 9, None, 8, None) == -1
 
 
 def test_workspace_and_state_sizes(lib):

@@ -24,6 +24,8 @@ CASES = [
     ((9, 100), 1, np.float64, (10,), 4),            # 1 value axis
     ((2, 128, 64), 1, np.float32, (128, 64), 0),    # one chunk: plan = vshape
     ((3, 4, 4), 1, np.complex128, (2, 2), 1),       # 16-B elements: strided path only
+    ((2, 128, 100), 1, np.float32, (32, 25), 1),    # 51 KiB records: staged in parts (GPU)
+    ((3, 3, 90, 60), 2, np.float64, (16, 16), 2),   # 43 KiB records, ragged chunks, parts
 ]
 
 
