@@ -3,20 +3,23 @@
 // One primitive, bm_copy_strided, serves every record-moving call site of
 // bolt's Spark path (see include/bolt_mi355x.h).  The host side reduces an
 // arbitrary N-d strided copy to a canonical form (unit dims dropped, dims
-// ordered by destination stride, mergeable neighbours fused) and picks one of
-// three kernels:
+// ordered by destination stride, mergeable neighbours fused) and picks:
 //
 //   rowcopy    innermost dim contiguous on both sides (a permutation that
-//              keeps the last axis, chunk pack/unpack of row bands): rows
-//              moved with 16-B vectors, 4 vectors in flight per lane.
+//              keeps the last axis, chunk pack/unpack of row bands): one 16-B
+//              vector per lane, a block per 256 vectors.
+//   runs       a kept inner run of 32-64 B with the two axes around it
+//              swapped: a tile transpose of 16-B-unit "super elements".
 //   transpose  the destination-contiguous dim differs from the source-
-//              contiguous one (swap / .T on the innermost axis): 64x64-element
+//              contiguous one (swap / .T on the innermost axis): TA x TB
 //              tiles staged through LDS (row pad of one element breaks the
 //              power-of-two bank stride), 16-B global loads along the source
-//              axis and 16-B stores along the destination axis.
+//              axis and 16-B stores along the destination axis; the tile
+//              shape is picked per element size and extents (pick_tile);
+//              1- and 2-byte elements pack 4 / 2 rows per 32-bit LDS word.
 //   generic    anything else (no unit stride): one element per lane.
 //
-// All three are HBM-bound; algorithmic bytes = 2 * N * elem_bytes.
+// All are HBM-bound; algorithmic bytes = 2 * N * elem_bytes.
 #include "bm_common.h"
 #include "../../include/bolt_mi355x.h"
 
