@@ -27,6 +27,13 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: grid * block threads < 2^32
+#ifndef BM_COLS_UNROLL
+#define BM_COLS_UNROLL 4  // rows in flight per lane in the column reductions (A/B knob)
+#endif
+#ifndef BM_COLS_BLOCKS
+#define BM_COLS_BLOCKS 2048  // split R over blocks below this many column tiles (A/B knob)
+#endif
+constexpr int kColsUnroll = BM_COLS_UNROLL;
 #ifndef BM_ROWS_UNROLL
 #define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
 #endif
@@ -274,6 +281,22 @@ __global__ void __launch_bounds__(kThreads)
       vload<T, VEC>(base + r_lo * d.I, k0);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc[k].pivot(to_f64(k0[k]));
+    }
+    if constexpr (MODE == M_MEAN || MODE == M_MOM || MODE == M_FSUM) {
+      // kColsUnroll rows in flight per lane; the adds stay in row order
+      for (; r + (kColsUnroll - 1) * nph < r_hi; r += kColsUnroll * nph) {
+        T v[kColsUnroll][VEC];
+#pragma unroll
+        for (int u = 0; u < kColsUnroll; ++u) vload_nt<T, VEC>(base + (r + u * nph) * d.I, v[u]);
+#pragma unroll
+        for (int u = 0; u < kColsUnroll; ++u) {
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            if (MODE == M_FSUM) fs[k] += to_f64(v[u][k]);
+            else acc[k].add(to_f64(v[u][k]));
+          }
+        }
+      }
     }
     for (; r + 3 * nph < r_hi; r += 4 * nph) {
       T v0[VEC], v1[VEC], v2[VEC], v3[VEC];
@@ -570,8 +593,8 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
     p.ntc = cdiv(ncolv, tcv);
     const int64_t blocks = O * p.ntc;
     int64_t nch = 1;
-    if (blocks < 2048) {
-      nch = cdiv(2048, blocks);
+    if (blocks < BM_COLS_BLOCKS) {
+      nch = cdiv(BM_COLS_BLOCKS, blocks);
       const int64_t maxch = std::max<int64_t>(1, R / ((int64_t)p.nph * 8));
       nch = std::min(nch, maxch);
     }

@@ -111,6 +111,8 @@ OPS = {
     "u8_T": lambda: Permute((2000, 1024, 2048), (2, 1, 0), np.uint8),
     "u16_2d": lambda: Permute((2000, 1048576), (1, 0), np.uint16),
     "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
+    "t64_mean_cols": lambda: Reduce(0, 1, 4096, 2097152, np.float32, np.float32),
+    "t64_std_cols": lambda: Reduce(2, 1, 4096, 2097152, np.float32, np.float32),
     "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
     "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),
     "c5_perm": lambda: Permute((64, 64, 64, 64, 64), (2, 0, 4, 1, 3), np.float64),
