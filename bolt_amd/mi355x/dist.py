@@ -170,6 +170,11 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
         n = qhi - qlo
         return qlo + k * n // K, qlo + (k + 1) * n // K
 
+    # equal slabs on every rank (the weak-scaling benches): one pack and one
+    # unpack launch per stage instead of one per peer
+    even_out = G > 1 and out_shape[0] % G == 0
+    even_in = G > 1 and shape[0] % G == 0
+
     with _phase("exchange", data.device):
         pending = None
         for k in range(K):
@@ -182,12 +187,20 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
                 parts.append((slo_q, bshape))
                 send_sizes.append(int(np.prod(bshape)) * es)
             send = _empty(sum(send_sizes), data.device)
-            off = 0
-            for (slo_q, bshape), nb in zip(parts, send_sizes):
-                if nb:
-                    backend.copy_strided(data, slo_q * sin[a] * es, send, off, bshape, sstr,
-                                         contiguous_strides(bshape), es)
-                off += nb
+            if even_out and send_sizes[0]:
+                # every peer's block has one shape and the sources are evenly
+                # spaced along axis a: the G packs are one strided copy
+                bshape = parts[0][1]
+                backend.copy_strided(data, parts[0][0] * sin[a] * es, send, 0, [G] + bshape,
+                                     [(parts[1][0] - parts[0][0]) * sin[a]] + sstr,
+                                     [send_sizes[0] // es] + contiguous_strides(bshape), es)
+            else:
+                off = 0
+                for (slo_q, bshape), nb in zip(parts, send_sizes):
+                    if nb:
+                        backend.copy_strided(data, slo_q * sin[a] * es, send, off, bshape, sstr,
+                                             contiguous_strides(bshape), es)
+                    off += nb
             mlo, mhi = sub(r, k)
             recv_sizes, rparts = [], []
             for s_ in range(G):
@@ -199,22 +212,30 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
                 recv_sizes.append(int(np.prod(bshape)) * es)
             recv, work = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(es), async_op=True)
             if pending is not None:
-                _unpack(backend, pending, out, tstr, j, es)
+                _unpack(backend, pending, out, tstr, j, es, even_in)
             pending = (recv, work, send, rparts, recv_sizes, mlo - lo)
-        _unpack(backend, pending, out, tstr, j, es)
+        _unpack(backend, pending, out, tstr, j, es, even_in)
     return out
 
 
-def _unpack(backend, pending, out, tstr, j, es):
+def _unpack(backend, pending, out, tstr, j, es, even=False):
     recv, work, send, rparts, recv_sizes, row0 = pending
     if work is not None:
         work.wait()  # the current stream waits for this stage's all-to-all
-    off = 0
-    for (slo, bshape), nb in zip(rparts, recv_sizes):
-        if nb:
-            backend.copy_strided(recv, off, out, (row0 * tstr[0] + slo * tstr[j]) * es, bshape,
-                                 contiguous_strides(bshape), tstr, es)
-        off += nb
+    if even and recv_sizes[0]:
+        # equal blocks from every rank, landing evenly spaced along axis j: one copy
+        slo, bshape = rparts[0]
+        G = len(rparts)
+        backend.copy_strided(recv, 0, out, (row0 * tstr[0] + slo * tstr[j]) * es, [G] + bshape,
+                             [recv_sizes[0] // es] + contiguous_strides(bshape),
+                             [(rparts[1][0] - slo) * tstr[j]] + tstr, es)
+    else:
+        off = 0
+        for (slo, bshape), nb in zip(rparts, recv_sizes):
+            if nb:
+                backend.copy_strided(recv, off, out, (row0 * tstr[0] + slo * tstr[j]) * es, bshape,
+                                     contiguous_strides(bshape), tstr, es)
+            off += nb
     del send
 
 
