@@ -2,19 +2,27 @@
 
 The reference moves records driver -> executors with parallelize
 (spark/construct.py:69) and back with collect (array.py:1012-1014).  Here the
-path is PCIe (63 GB/s spec, MI355X_MICROARCH.md): a pageable copy bounces
-through the driver's own staging buffers, so large arrays are staged through
-two page-locked chunks from torch's caching host allocator -- the host memcpy
-of chunk i+1 (split over a few threads; numpy releases the GIL) overlaps the
-DMA of chunk i on the current stream.  Small transfers take one pinned buffer.
+path is PCIe (63 GB/s spec, MI355X_MICROARCH.md).
+
+Ingest: the runtime's own pageable copy reaches 56 GB/s on the box, ahead of
+staging through page-locked chunks (54 GB/s at 8 copy threads,
+profiles/r01_transfer_*.log), so it is the default (BOLT_AMD_H2D=staged
+selects the staged path).  Egress: a pageable D2H bounces through the
+driver's staging at 6-8 GB/s, so large results are staged through two
+page-locked chunks from torch's caching host allocator -- the host memcpy of
+chunk i (split over 8 threads; numpy releases the GIL) overlaps the DMA of
+chunk i+1 -- 17-18 GB/s, bound by first-touch page faults of the fresh numpy
+result.  Small transfers take one pinned buffer and return a view of it.
 """
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-CHUNK = 64 << 20          # bytes per staging chunk
+CHUNK = int(os.environ.get("BOLT_AMD_COPY_CHUNK_MB", "64")) << 20   # bytes per staging chunk
 SMALL = 8 << 20           # below this: one pinned buffer, no pipeline
-THREADS = 4               # host memcpy threads per chunk
+THREADS = int(os.environ.get("BOLT_AMD_COPY_THREADS", "8"))        # host memcpy threads per chunk
+H2D_DIRECT = os.environ.get("BOLT_AMD_H2D", "direct") == "direct"  # the runtime's pageable copy
 
 _POOL = None
 
@@ -45,6 +53,8 @@ def to_device(host, device):
     if device.type != "cuda":
         return torch.from_numpy(host.copy())
     n = host.size
+    if H2D_DIRECT:
+        return torch.from_numpy(host).to(device)
     out = torch.empty(n, dtype=torch.uint8, device=device)
     if n == 0:
         return out
