@@ -85,7 +85,10 @@ def test_transpose_full_size_c3_c5(gpu_ctx):
     import torch
     for shape, dtype, split, perm in [((4096, 256, 256, 32), np.float32, 2, (3, 2, 1, 0)),
                                       ((64,) * 5, np.float64, 3, (4, 3, 2, 1, 0)),
-                                      ((64,) * 5, np.float64, 3, (2, 0, 4, 1, 3))]:
+                                      ((64,) * 5, np.float64, 3, (2, 0, 4, 1, 3)),
+                                      # C4's uint16 reversed: packed-word tiles (k_transpose_pk)
+                                      ((10000, 1024, 1024), np.uint16, 1, (2, 1, 0)),
+                                      ((2000, 1024, 2048), np.uint8, 1, (2, 1, 0))]:
         b, raw = _shard(gpu_ctx, shape, dtype, split, 3)
         t = b.transpose(perm)
         _sample_check(raw, shape, dtype, t, perm)
