@@ -54,6 +54,9 @@ constexpr int kThreads = 256;
 #ifndef BM_RC_XCD
 #define BM_RC_XCD 0  // XCD-grouped covering grid: +5% in a C4 microbench (r01_rc1) but -3..-20% in the product A/B (r01_ab_rc)
 #endif
+#ifndef BM_GEN_GRIDCAP
+#define BM_GEN_GRIDCAP 4096  // generic copies: grid-stride (uncapped measured -20% on reversed slices, r01_index2)
+#endif
 #ifndef BM_RUNS_T
 #define BM_RUNS_T 1
 #endif
@@ -607,7 +610,7 @@ int launch_generic(const char *src, char *dst, const std::vector<Dim> &dims, int
   }
   uint64_t total = 1;
   for (const Dim &x : dims) total *= (uint64_t)x.n;
-  const int grid = grid_for(total, kThreads);
+  const int grid = grid_for(total, kThreads, BM_GEN_GRIDCAP);
   switch (es) {
     case 1: k_generic<1><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
     case 2: k_generic<2><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;

@@ -122,7 +122,10 @@ class HipBackend(object):
             return
         if idx.min() < 0 or idx.max() >= src_rows:
             raise IndexError("gather index out of range [0, %d)" % src_rows)
-        didx = torch.from_numpy(idx).to(src.device, non_blocking=False)
+        # page-locked + non-blocking: the upload queues behind earlier kernels
+        # without blocking the host (the caching host allocator keeps the
+        # pinned block until the copy has run)
+        didx = torch.from_numpy(idx).pin_memory().to(src.device, non_blocking=True)
         _lib.check(self.lib.bm_gather_rows(self._ptr(src, src_off), self._ptr(dst, dst_off), int(n_outer),
                                            int(src_rows), int(row_bytes), ctypes.c_void_p(didx.data_ptr()),
                                            int(idx.size), self._stream(src)), "bm_gather_rows")

@@ -456,7 +456,10 @@ class BoltArrayMI355X(BoltArray):
             taken = self._like(data, tuple(newshape), self._split)
             rest = list(index)
             rest[loc] = slice(0, None, None)
-            result = taken[tuple(rest)]
+            full = all(isinstance(r, slice) and r.step in (None, 1) and (r.start or 0) == 0 and
+                       (r.stop is None or r.stop >= d) for r, d in zip(rest, taken.shape))
+            # the other axes untouched: the gathered array is the result (no second copy)
+            result = taken if full and not int_locs else taken[tuple(rest)]
         if len(int_locs) == self.ndim:
             return result.toarray().reshape(())[()]
         return result.squeeze(tuple(int_locs)) if int_locs else result

@@ -138,11 +138,10 @@ def advanced_points(index, shape, split):
 def mixed_take(index, shape, split):
     """(loc, idx) of the single list index (array.py:561-593)."""
     loc = [i for i, x in enumerate(index) if isinstance(x, np.ndarray)][0]
-    idx = list(index[loc])
-    if isinstance(idx[0], (tuple, list, np.ndarray)):
+    idx = np.asarray(index[loc])
+    if idx.ndim != 1 or idx.dtype == object:  # a nested sequence (the reference checks idx[0])
         raise ValueError("When mixing basic and advanced indexing, "
                          "advanced index must be one-dimensional")
-    idx = np.asarray(idx)
     if idx.dtype.kind not in "iu":
         raise ValueError("indices must be integers")
     idx = idx.astype(np.int64)

@@ -21,7 +21,9 @@ def timed(f, reps=5):
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
+    out = None
     for _ in range(reps):
+        out = None  # free the previous result first: one live output, no allocator churn
         out = f()
     e1.record()
     e1.synchronize()
