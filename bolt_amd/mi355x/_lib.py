@@ -13,7 +13,8 @@ ABI_VERSION = 1
 BM_BOOL, BM_U8, BM_I8, BM_U16, BM_I16, BM_U32, BM_I32, BM_U64, BM_I64, BM_F16, BM_F32, BM_F64 = range(12)
 STAT_MEAN, STAT_VAR, STAT_STD, STAT_SUM, STAT_MAX, STAT_MIN = range(6)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libbolt_mi355x.so")
+LIB_PATH = os.environ.get("BOLT_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libbolt_mi355x.so")  # env: A/B builds
 
 # every symbol include/bolt_mi355x.h declares: name -> (restype, argtypes)
 _c = ctypes
