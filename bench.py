@@ -216,10 +216,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not the measured configuration): several ranks on one
+    # GPU over gloo, exchanges staged through the host
+    backend = os.environ.get("BOLT_AMD_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("BOLT_AMD_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import bolt_amd as bolt
     from bolt_amd import MI355XContext
@@ -294,7 +301,7 @@ def main():
             phases[k] = float(np.mean([a.elapsed_time(z) for a, z in evs]))
         bdist.PROFILE = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -321,6 +328,8 @@ def main():
         "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
         "config": {"workload": desc, "global_shape": list(gshape), "split": split,
                    "parallelism": "dp%d (records sharded on the leading key axis)" % world,
+                   "collectives": "RCCL (torch.distributed nccl)" if backend == "nccl" or world == 1
+                                  else "%s, host-staged (one-GPU rehearsal, not a measurement)" % backend,
                    "bytes_per_step": {k: int(v) for k, v in per.items()}},
         "roofline": {
             "bound": "hbm",
