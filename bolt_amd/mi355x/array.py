@@ -23,7 +23,7 @@ import numpy as np
 from bolt_amd.mi355x import _lib
 from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
-from bolt_amd.mi355x.context import contiguous_strides, local_shape
+from bolt_amd.mi355x.context import local_shape
 from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, permute_sharded, redistribute_rows, select_sharded, _empty
 from bolt_amd.mi355x.transfer import to_device, to_host
 from bolt_amd.local import BoltArrayLocal
