@@ -620,9 +620,14 @@ class BoltArrayMI355X(BoltArray):
 
         if name and not func:
             inshape(self.shape, axis)
-            arr, _ = self._reduced(axis, _STAT_CODES[name])
-            if arr.ndim == 0:
-                arr = arr[()]
+            if self._nrecords(axis) == 0:
+                # no records after _align: the merged StatCounter is the empty one
+                # (statcounter.py:28-41, :109-130): mean 0.0, variance / stdev nan
+                arr = 0.0 if name == 'mean' else float('nan')
+            else:
+                arr, _ = self._reduced(axis, _STAT_CODES[name])
+                if arr.ndim == 0:
+                    arr = arr[()]
             if keepdims:
                 for i in axis:
                     arr = np.expand_dims(arr, axis=i)
@@ -644,6 +649,8 @@ class BoltArrayMI355X(BoltArray):
             raise NotImplementedError("the mi355x mode reduces with add / maximum / minimum; got %r" % (func,))
         axis = tupleize(axis)
         inshape(self.shape, axis)
+        if self._nrecords(axis) == 0:
+            raise ValueError("Can not reduce() empty RDD")  # treeReduce of no records (array.py:269)
         arr, _ = self._reduced(axis, stat)
         if arr.ndim == 0:
             arr = arr[()]
@@ -655,6 +662,10 @@ class BoltArrayMI355X(BoltArray):
         elif arr.shape == (1,):
             return arr[0]
         return BoltArrayLocal(arr)
+
+    def _nrecords(self, axis):
+        """Records the reduction sees after _align: the product of the reduced extents."""
+        return int(np.prod([self._shape[int(a)] for a in axis], dtype=np.int64))
 
     def mean(self, axis=None, keepdims=False):
         """Mean over ``axis`` (array.py:336-349)."""

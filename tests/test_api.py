@@ -226,3 +226,23 @@ def test_stats_dtypes(bctx):
     sm = bu.sum(axis=0)
     assert sm.dtype == np.uint16
     assert exact(np.asarray(sm), np.add.reduce(u, axis=0, dtype=np.uint16))
+
+
+def test_empty_reductions(bctx):
+    """Reductions over zero records follow the reference's StatCounter / treeReduce
+    (statcounter.py:28-130, array.py:243-334): an empty StatCounter gives mean
+    0.0 and variance / stdev nan; reduce() of no records raises ValueError.
+    Axes with records but empty values give empty results of the kept shape."""
+    import math
+    b = bolt.array(np.zeros((0, 3, 4), np.float32), bctx)
+    assert b.mean(axis=0) == 0.0
+    assert math.isnan(b.var(axis=0)) and math.isnan(b.std(axis=0))
+    with pytest.raises(ValueError):
+        b.sum(axis=0)
+    with pytest.raises(ValueError):
+        b.max(axis=0)
+    assert b.mean(axis=1).shape == (0, 4) and b.sum(axis=(1,)).shape == (0, 4)
+    c = bolt.array(np.zeros((3, 0, 4), np.float32), bctx)
+    assert c.mean(axis=0).shape == (0, 4) and c.std(axis=0).shape == (0, 4)
+    assert c.swap((0,), (0,)).shape == (0, 3, 4)
+    assert exact(c.T.toarray(), np.zeros((4, 0, 3), np.float32))
