@@ -57,6 +57,9 @@ constexpr int kThreads = 256;
 #ifndef BM_GEN_GRIDCAP
 #define BM_GEN_GRIDCAP 4096  // generic copies: grid-stride (uncapped measured -20% on reversed slices, r01_index2)
 #endif
+#ifndef BM_FUSE
+#define BM_FUSE 1  // fuse short contiguous transpose axes with their continuation (A/B knob)
+#endif
 #ifndef BM_RUNS_T
 #define BM_RUNS_T 1
 #endif
@@ -113,6 +116,13 @@ struct TransDesc {
   FastDiv ntAB;    // tiles per batch element
   uint64_t ntiles; // total tiles
   Decomp batch;    // remaining dims
+  // fused pairs (FUSED kernels): b = b_hi * Lb1 + b_lo is contiguous in the
+  // destination but reads source rows at b_lo * sb + b_hi * sb2; a = a_hi *
+  // La1 + a_lo is contiguous in the source and writes destination rows at
+  // a_lo * da + a_hi * da2.  Short extents (C5's 64-wide axes) then still get
+  // long tile rows.
+  FastDiv Lb1, La1;
+  int64_t sb2, da2;
 };
 
 // TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
@@ -122,7 +132,21 @@ struct TransDesc {
 // first LDS write, so a block keeps TB*TA*sizeof(T) bytes in flight
 // (tools/microbench/transpose_tiles.hip: +6% at 64x256 f32 over writing
 // each load to LDS as it lands).
-template <typename T, int TA, int TB, int VA, int VB>
+template <bool FUSED>
+__device__ __forceinline__ int64_t brow(const TransDesc &d, int64_t b) {
+  if (!FUSED) return b * d.sb;
+  const int64_t hi = (int64_t)fd_div((uint64_t)b, d.Lb1);
+  return (b - hi * (int64_t)d.Lb1.d) * d.sb + hi * d.sb2;
+}
+
+template <bool FUSED>
+__device__ __forceinline__ int64_t arow(const TransDesc &d, int64_t a) {
+  if (!FUSED) return a * d.da;
+  const int64_t hi = (int64_t)fd_div((uint64_t)a, d.La1);
+  return (a - hi * (int64_t)d.La1.d) * d.da + hi * d.da2;
+}
+
+template <typename T, int TA, int TB, int VA, int VB, bool FUSED = false>
 __global__ void __launch_bounds__(kThreads)
     k_transpose(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
   __shared__ T tile[TB][TA + 1];
@@ -156,7 +180,7 @@ __global__ void __launch_bounds__(kThreads)
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
 
     // load: lanes walk dim a (source-contiguous); all loads in flight first
-    const T *s = src + so + a0 + b0 * d.sb;
+    const T *s = src + so + a0;
     const bool fullA = (a0 + ia + VA <= d.La);
 #pragma unroll
     for (int i0 = 0; i0 < NL; i0 += NLB) {
@@ -165,7 +189,7 @@ __global__ void __launch_bounds__(kThreads)
       for (int j = 0; j < NLB; ++j) {
         const int rb = ty + (i0 + j) * RPA;
         if (b0 + rb < d.Lb) {
-          const T *p = s + ia + (int64_t)rb * d.sb;
+          const T *p = s + ia + brow<FUSED>(d, b0 + rb);
           if (fullA) {
             vload_nt<T, VA>(p, v[j]);
           } else {
@@ -184,7 +208,7 @@ __global__ void __launch_bounds__(kThreads)
     __syncthreads();
 
     // store: lanes walk dim b (destination-contiguous)
-    T *q = dst + dof + b0 + a0 * d.da;
+    T *q = dst + dof + b0;
     const bool fullB = (b0 + ib + VB <= d.Lb);
 #pragma unroll
     for (int it = 0; it < NS; ++it) {
@@ -193,7 +217,7 @@ __global__ void __launch_bounds__(kThreads)
         T w[VB];
 #pragma unroll
         for (int k = 0; k < VB; ++k) w[k] = tile[ib + k][ra];
-        T *p = q + (int64_t)ra * d.da + ib;
+        T *p = q + arow<FUSED>(d, a0 + ra) + ib;
         if (fullB) {
           vstore_nt<T, VB>(p, w);
         } else {
@@ -465,8 +489,14 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
 
 template <typename T, int TA, int TB>
 void launch_transpose_tile(const T *src, T *dst, const TransDesc &td, bool va_vec, bool vb_vec, int grid,
-                           hipStream_t st) {
+                           bool fused, hipStream_t st) {
   constexpr int W = 16 / (int)sizeof(T);
+  if constexpr (sizeof(T) >= 4) {
+    if (fused) {  // fused axis pairs: vectorised only (the host fuses aligned layouts)
+      k_transpose<T, TA, TB, W, W, true><<<grid, kThreads, 0, st>>>(src, dst, td);
+      return;
+    }
+  }
   if (va_vec && vb_vec)
     k_transpose<T, TA, TB, W, W><<<grid, kThreads, 0, st>>>(src, dst, td);
   else if (va_vec)
@@ -489,12 +519,12 @@ constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {32, 64}, {64, 64}, {64, 32}, 
 
 template <typename T>
 int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool va_vec, bool vb_vec,
-                       hipStream_t st) {
+                       bool fused, hipStream_t st) {
   uint64_t g = td.ntiles;
   if (g > kMaxGrid) g = kMaxGrid;  // grid-stride beyond the launch limit
   const int grid = (int)g;
 #define BM_TILE(A, B) \
-  if (tl.ta == A && tl.tb == B) { launch_transpose_tile<T, A, B>(src, dst, td, va_vec, vb_vec, grid, st); return BM_OK; }
+  if (tl.ta == A && tl.tb == B) { launch_transpose_tile<T, A, B>(src, dst, td, va_vec, vb_vec, grid, fused, st); return BM_OK; }
   if constexpr (sizeof(T) == 1) {
     BM_TILE(128, 256) BM_TILE(128, 128) BM_TILE(64, 64) BM_TILE(256, 64) BM_TILE(64, 256)
   } else if constexpr (sizeof(T) == 2) {
@@ -542,7 +572,7 @@ Tile pick_tile(int64_t La, int64_t Lb, int es) {
 }
 
 int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, int a, int es,
-                     hipStream_t st) {
+                     hipStream_t st, bool allow_fuse = true) {
   const int b = (int)dims.size() - 1;
   std::vector<Dim> batch;
   for (int k = 0; k < (int)dims.size(); ++k)
@@ -552,6 +582,40 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   td.Lb = dims[b].n;
   td.sb = dims[b].ss;
   td.da = dims[a].ds;
+  td.Lb1 = make_fastdiv((uint64_t)td.Lb);
+  td.La1 = make_fastdiv((uint64_t)td.La);
+  td.sb2 = 0;
+  td.da2 = 0;
+  // Short contiguous axes: fuse b with the dim that continues it in the
+  // destination (ds == Lb) and a with the dim that continues it in the source
+  // (ss == La), so tile rows stay >= 512 B / 256 B (C3 .T: 128-B source rows,
+  // +21%, profiles/r01_ab_fuse.log).
+  bool fused = false;
+  if (BM_FUSE && allow_fuse && es >= 4 && aligned(src, 16) && aligned(dst, 16)) {
+    auto take = [&](bool want_b) -> int {
+      for (int k = 0; k < (int)batch.size(); ++k)
+        if (want_b ? batch[k].ds == td.Lb : batch[k].ss == td.La) return k;
+      return -1;
+    };
+    if (td.Lb * es < 512) {  // (C5's 512-B rows: fusing measured -10%, profiles/r01_ab_fuse.log)
+      const int k = take(true);
+      if (k >= 0) {
+        td.sb2 = batch[k].ss;
+        td.Lb *= batch[k].n;
+        batch.erase(batch.begin() + k);
+        fused = true;
+      }
+    }
+    if (td.La * es < 256) {
+      const int k = take(false);
+      if (k >= 0) {
+        td.da2 = batch[k].ds;
+        td.La *= batch[k].n;
+        batch.erase(batch.begin() + k);
+        fused = true;
+      }
+    }
+  }
   if (!fill_decomp(td.batch, batch)) {
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
     return BM_E_ARG;
@@ -572,6 +636,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     if (k != a && (dims[k].ss * es) % 16) va = false;
     if (k != b && (dims[k].ds * es) % 16) vb = false;
   }
+  if (fused && !(va && vb && (td.Lb1.d * es) % 16 == 0 && (td.La1.d * es) % 16 == 0)) {
+    // the fused kernels are vectorised only: the plain tiles handle it
+    return launch_transpose(src, dst, dims, a, es, st, false);
+  }
   if (BM_PK && va && vb && (es == 1 || es == 2)) {
     // packed-word tiles: 128-B source and 1-KiB destination segments
     const int ta = es == 2 ? BM_PK16_TA : BM_PK8_TA, tbb = es == 2 ? BM_PK16_TB : BM_PK8_TB;
@@ -591,10 +659,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     return BM_OK;
   }
   switch (es) {
-    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, st);
-    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, st);
-    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, st);
-    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, st);
+    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, false, st);
+    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, false, st);
+    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, fused, st);
+    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, fused, st);
     default: break;
   }
   bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);

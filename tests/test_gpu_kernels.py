@@ -80,6 +80,13 @@ def test_permute_all_perms_4d(dtype):
     ((528, 2, 144), (2, 1, 0)),
     ((1040, 3, 96), (2, 1, 0)),
     ((48, 1600), (1, 0)),
+    # short 16-B aligned axes fused with their continuation (TransDesc Lb1/La1)
+    ((100, 24, 16), (2, 1, 0)),
+    ((8, 64, 64, 64), (3, 2, 1, 0)),
+    ((32, 16, 48, 8), (3, 2, 1, 0)),
+    ((12, 20, 36), (2, 0, 1)),
+    ((4, 8, 12, 16, 20), (4, 3, 2, 1, 0)),
+    ((16, 16, 16, 16), (2, 3, 0, 1)),
 ])
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64, np.complex128])
 def test_permute_shapes(shape, perm, dtype):
