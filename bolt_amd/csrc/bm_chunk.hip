@@ -48,6 +48,38 @@ struct Parts {
   int64_t dlo[kMaxParts], dhi[kMaxParts], slo[kMaxParts], shi[kMaxParts];
 };
 
+// Stage n L-vectors of a contiguous source range into LDS, kStageU loads in
+// flight per lane (a one-load-then-wait loop left the kernel latency-bound).
+#ifndef BM_STAGE_U
+#define BM_STAGE_U 8
+#endif
+#ifndef BM_GATHER_U
+#define BM_GATHER_U 0  // 0: 16 B of map per lane per round
+#endif
+constexpr int kStageU = BM_STAGE_U;
+template <typename L>
+__device__ __forceinline__ void stage_lds(L *sl, const L *s, int64_t n) {
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)kStageU * kCThreads) {
+    L v[kStageU];
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int64_t i = i0 + (int64_t)u * kCThreads;
+      if (i < n) v[u] = __builtin_nontemporal_load(s + i);
+    }
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int64_t i = i0 + (int64_t)u * kCThreads;
+      if (i < n) sl[i] = v[u];
+    }
+  }
+}
+
+// destination vectors per lane per gather round: their map reads go out together
+template <int VEC>
+struct GatherU {
+  static constexpr int v = BM_GATHER_U > 0 ? BM_GATHER_U : (VEC >= 8 ? 2 : 16 / VEC);
+};
+
 // LB: staging load width in bytes (16 when the tile's bytes are 16-B aligned)
 template <int ES, int VEC, int LB>
 __global__ void __launch_bounds__(kCThreads)
@@ -63,25 +95,40 @@ __global__ void __launch_bounds__(kCThreads)
     const int64_t r0 = t * rb;
     const int64_t nr = min(rb, nrec - r0);
     // stage nr contiguous source records
-    const int64_t nld = nr * src_rec * ES / LB;
-    const L *s = reinterpret_cast<const L *>(src + r0 * src_rec * ES);
-    L *sl = reinterpret_cast<L *>(smem);
-    for (int64_t i = threadIdx.x; i < nld; i += kCThreads) sl[i] = __builtin_nontemporal_load(s + i);
+    stage_lds(reinterpret_cast<L *>(smem), reinterpret_cast<const L *>(src + r0 * src_rec * ES),
+              nr * src_rec * ES / LB);
     __syncthreads();
-    // gather nr destination records, VEC elements per lane
+    // gather nr destination records, VEC elements per lane, GU vectors per round
+    constexpr int GU = GatherU<VEC>::v;
     const int64_t nout = nr * dst_rec / VEC;
     V *d = reinterpret_cast<V *>(dst + r0 * dst_rec * ES);
-    for (int64_t i = threadIdx.x; i < nout; i += kCThreads) {
-      const uint64_t e = (uint64_t)i * VEC;
-      const uint64_t r = fd_div(e, fdst);
-      const int64_t o = (int64_t)(e - r * fdst.d);
-      const T *rl = lds + r * src_rec;
-      T v[VEC];
+    for (int64_t i0 = threadIdx.x; i0 < nout; i0 += (int64_t)GU * kCThreads) {
+      int32_t m[GU][VEC];
+      int64_t rb_[GU];
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) v[k] = rl[map[o + k]];
-      V w;
-      __builtin_memcpy(&w, v, sizeof(V));
-      __builtin_nontemporal_store(w, d + i);
+      for (int u = 0; u < GU; ++u) {
+        const int64_t i = i0 + (int64_t)u * kCThreads;
+        if (i < nout) {
+          const uint64_t e = (uint64_t)i * VEC;
+          const uint64_t r = fd_div(e, fdst);
+          const int64_t o = (int64_t)(e - r * fdst.d);
+          rb_[u] = (int64_t)r * src_rec;
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) m[u][k] = map[o + k];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int64_t i = i0 + (int64_t)u * kCThreads;
+        if (i < nout) {
+          T v[VEC];
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) v[k] = lds[rb_[u] + m[u][k]];
+          V w;
+          __builtin_memcpy(&w, v, sizeof(V));
+          __builtin_nontemporal_store(w, d + i);
+        }
+      }
     }
     __syncthreads();
   }
@@ -102,21 +149,35 @@ __global__ void __launch_bounds__(kCThreads)
     const int64_t r = t / P.n;
     const int p = (int)(t - r * P.n);
     const int64_t slo = P.slo[p], dlo = P.dlo[p];
-    const int64_t nld = (P.shi[p] - slo) * ES / LB;
-    const L *s = reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES);
-    L *sl = reinterpret_cast<L *>(smem);
-    for (int64_t i = threadIdx.x; i < nld; i += kCThreads) sl[i] = __builtin_nontemporal_load(s + i);
+    stage_lds(reinterpret_cast<L *>(smem), reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES),
+              (P.shi[p] - slo) * ES / LB);
     __syncthreads();
+    constexpr int GU = GatherU<VEC>::v;
     const int64_t nout = (P.dhi[p] - dlo) / VEC;
     V *d = reinterpret_cast<V *>(dst + (r * dst_rec + dlo) * ES);
-    for (int64_t i = threadIdx.x; i < nout; i += kCThreads) {
-      const int64_t o = dlo + i * VEC;
-      T v[VEC];
+    const int32_t *mp = map + dlo;
+    for (int64_t i0 = threadIdx.x; i0 < nout; i0 += (int64_t)GU * kCThreads) {
+      int32_t m[GU][VEC];
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) v[k] = lds[map[o + k] - slo];
-      V w;
-      __builtin_memcpy(&w, v, sizeof(V));
-      __builtin_nontemporal_store(w, d + i);
+      for (int u = 0; u < GU; ++u) {
+        const int64_t i = i0 + (int64_t)u * kCThreads;
+        if (i < nout) {
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) m[u][k] = mp[i * VEC + k];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GU; ++u) {
+        const int64_t i = i0 + (int64_t)u * kCThreads;
+        if (i < nout) {
+          T v[VEC];
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) v[k] = lds[m[u][k] - slo];
+          V w;
+          __builtin_memcpy(&w, v, sizeof(V));
+          __builtin_nontemporal_store(w, d + i);
+        }
+      }
     }
     __syncthreads();
   }

@@ -42,7 +42,11 @@ def dtype_code(dtype):
         raise NotImplementedError("statistics over dtype %s are not supported by the mi355x mode" % dt)
 
 
-PART_BYTES = 24576  # LDS per (record, part) tile of bm_record_gather: 6 blocks per CU
+# Records up to PART_BYTES are staged whole (5 blocks per CU); larger ones are
+# split into (record, part) tiles.  C5: the 32-KiB pack record whole 3.26 ms
+# vs parts 3.45; the 46-KiB values_to_keys record parts 3.72 vs whole 3.85
+# (profiles/r01_ab_recmap2.log)
+PART_BYTES = 32768
 
 
 def record_parts(rmap, src_rec, es, part_bytes=None):

@@ -28,6 +28,9 @@ def load(path):
                               ctypes.c_size_t, ctypes.c_void_p]
     lib.bm_reduce_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                               ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]
+    lib.bm_record_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, I64P, ctypes.c_int,
+                                     ctypes.c_void_p]
     lib.bm_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -92,7 +95,43 @@ class Copy(object):
         assert rc == 0, lib.bm_last_error()
 
 
+class RecGather(object):
+    """C5's chunk pack ((16,16), padding 2 on 64x64 float64 records) or its
+    values_to_keys((0,)) repack, as one bm_record_gather (parts as _ops picks)."""
+
+    def __init__(self, kind, nparts_off=False):
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bolt_amd.mi355x import plan, _ops
+        geom = plan.ChunkGeometry((64, 64), (16, 16), (2, 2))
+        self.nrec = 64 ** 3
+        if kind == "pack":
+            rmap, self.src_rec = geom.record_map(unpack=False), 64 * 64
+        else:
+            vmask = np.array([True, False])
+            new = plan.ChunkGeometry((64,), (16,), (2,))
+            rmap = plan.copies_to_map(plan.v2k_copies(geom, new, [], vmask), 64 * new.size)
+            self.src_rec = geom.size
+        self.dst_rec = rmap.size
+        parts = [] if nparts_off else _ops.record_parts(rmap, self.src_rec, 8)
+        self.nparts, self.parts = len(parts) // 4, (i64(parts) if parts else None)
+        self.map = torch.from_numpy(rmap).cuda()
+        self.src = torch.randint(0, 255, (self.nrec * self.src_rec * 8,), dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty(self.nrec * self.dst_rec * 8, dtype=torch.uint8, device="cuda")
+        self.bytes = self.src.numel() + self.dst.numel()
+
+    def __call__(self, lib):
+        rc = lib.bm_record_gather(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
+                                  self.nrec, self.src_rec, self.dst_rec, ctypes.c_void_p(self.map.data_ptr()),
+                                  self.nparts, self.parts, 8, stream())
+        assert rc == 0, lib.bm_last_error()
+
+
 OPS = {
+    "c5_pack": lambda: RecGather("pack"),
+    "c5_pack_whole": lambda: RecGather("pack", True),
+    "c5_v2k": lambda: RecGather("v2k"),
+    "c5_v2k_whole": lambda: RecGather("v2k", True),
     "c2_copy": lambda: Copy(2097152000),
     "c2_swap": lambda: Permute((2000, 512 * 512), (1, 0), np.float32),
     "c2_mean_rows": lambda: Reduce(0, 512 * 512, 2000, 1, np.float32, np.float32),
