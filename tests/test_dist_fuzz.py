@@ -1,0 +1,75 @@
+"""The seeded oracle fuzz (tests/test_fuzz_oracle.py) on several ranks: world
+2 and 3 over gloo with the numpy test executor, and 2 ranks sharing cuda:0
+with the HIP kernels.  Random shapes give ragged and empty shards, swaps and
+transposes that exchange records (pack -> all_to_all -> unpack), chunked
+keys_to_values across ranks, and statistics over the sharded axis (per-rank
+states -> all_gather -> ordered Chan combine), each compared with the oracle.
+"""
+import os
+import traceback
+
+import pytest
+import torch.multiprocessing as mp
+
+from test_dist_gloo import _free_port
+
+SEEDS = range(0, 200, 4)
+
+
+def _worker(rank, world, port, errq, device):
+    import sys
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from bolt_amd import MI355XContext
+        if device == "cpu":
+            import cpu_backend
+            cpu_backend.install()
+        ctx = MI355XContext(device=device)
+        from test_fuzz_oracle import check_case
+        for seed in SEEDS:
+            try:
+                check_case(ctx, seed)
+            except Exception:
+                raise AssertionError("seed %d failed" % seed)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put((rank, traceback.format_exc()))
+        raise
+
+
+def _run(world, device):
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, errq, device)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_fuzz_gloo(world):
+    _run(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_dist_fuzz_gpu_kernels_one_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run(2, "cuda:0")

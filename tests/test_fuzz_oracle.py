@@ -50,6 +50,12 @@ def _records_equal(got, want):
 
 @pytest.mark.parametrize("seed", range(NCASES))
 def test_fuzz_against_oracle(bctx, seed):
+    check_case(bctx, seed)
+
+
+def check_case(bctx, seed):
+    """One seeded case on context ``bctx`` (also run per rank by
+    tests/test_dist_fuzz.py, where every collective path is exercised)."""
     rng, x, split = _case(seed)
     ndim = x.ndim
     axis = tuple(range(split))
