@@ -127,7 +127,31 @@ class RecGather(object):
         assert rc == 0, lib.bm_last_error()
 
 
+class K2V(object):
+    """C5's chunked keys_to_values((2,)) as the strided copies chunk.py runs
+    (plan.k2v_copies, packed -> packed: 3200-B rows of old chunk boxes)."""
+
+    def __init__(self):
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bolt_amd.mi355x import plan
+        old = plan.ChunkGeometry((64, 64), (16, 16), (2, 2))
+        new = plan.ChunkGeometry((64, 64, 64), (64, 16, 16), (0, 2, 2))
+        self.copies = plan.k2v_copies(old, new, [64, 64, 64], np.array([False, False, True]))
+        self.src = torch.randint(0, 255, (64 ** 3 * old.size * 8,), dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty(64 ** 2 * new.size * 8, dtype=torch.uint8, device="cuda")
+        self.bytes = self.src.numel() + self.dst.numel()
+        self.args = [(ctypes.c_void_p(self.src.data_ptr() + so * 8), ctypes.c_void_p(self.dst.data_ptr() + do * 8),
+                      len(sh), i64(sh), i64(ss), i64(ds)) for sh, ss, ds, so, do in self.copies]
+
+    def __call__(self, lib):
+        for a in self.args:
+            rc = lib.bm_copy_strided(*a, 8, stream())
+            assert rc == 0, lib.bm_last_error()
+
+
 OPS = {
+    "c5_k2v": lambda: K2V(),
     "c5_pack": lambda: RecGather("pack"),
     "c5_pack_whole": lambda: RecGather("pack", True),
     "c5_v2k": lambda: RecGather("v2k"),
