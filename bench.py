@@ -44,7 +44,7 @@ CONFIGS = {
            "+ float64 var over axis 0"),
     "C5": ((64, 64, 64, 64, 64), np.float64, 3,
            "C5: float64 64^5 per GPU, keys (0,1,2); .T + transpose(2,0,4,1,3) + "
-           "chunk((16,16), padding=2) -> unchunk"),
+           "chunk((16,16), padding=2) -> unchunk / keys_to_values((2,)) / values_to_keys((0,))"),
     "target64": ((8192, 256, 256, 32), np.float32, 2,
                  "64 GiB float32 4-D per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
 }
@@ -162,11 +162,16 @@ def steps_of(cfg, b, world=1):
     if cfg == "C5":
         from bolt_amd.mi355x.plan import ChunkGeometry
         P = ChunkGeometry(b.shape[3:], (16, 16), (2, 2)).size * (n // int(np.prod(b.shape[3:]))) * s
+        # values_to_keys((0,)): every record's 64 core rows become records of the
+        # remaining axis, chunked 16 with padding 2 (76 elements each)
+        Pv = ChunkGeometry(b.shape[4:], (16,), (2,)).size * b.shape[3] * (n // int(np.prod(b.shape[3:]))) * s
         ck = {}
         return [("T", lambda: b.T, 2 * N),
                 ("transpose", lambda: b.transpose(2, 0, 4, 1, 3), 2 * N),
                 ("chunk", lambda: ck.__setitem__("c", b.chunk((16, 16), padding=2)), N + P),
-                ("unchunk", lambda: ck.pop("c").unchunk(), P + N)]
+                ("unchunk", lambda: ck["c"].unchunk(), P + N),
+                ("keys_to_values", lambda: ck["c"].keys_to_values((2,)), 2 * P),
+                ("values_to_keys", lambda: ck.pop("c").values_to_keys((0,)), P + Pv)]
     raise ValueError(cfg)
 
 

@@ -83,6 +83,11 @@ def _body(rank, world):
             assert np.asarray(results["transpose"].toarray()).tobytes() == \
                 np.ascontiguousarray(full.transpose(2, 0, 4, 1, 3)).tobytes()
             assert np.asarray(results["unchunk"].toarray()).tobytes() == full.tobytes()
+            # both re-chunkings keep the axis order of this config
+            k2v, v2k = results["keys_to_values"], results["values_to_keys"]
+            assert k2v.split == 2 and v2k.split == 4
+            assert np.asarray(k2v.unchunk().toarray()).tobytes() == full.tobytes()
+            assert np.asarray(v2k.unchunk().toarray()).tobytes() == full.tobytes()
 
 
 def _worker(rank, world, port, errq):
