@@ -31,3 +31,26 @@ extern "C" int bm_device_cus(void) {
   }
   return cus;
 }
+
+// 1 if [p, p + bytes) is page-locked host memory the current device can store
+// to at the same address (ROCm maps hipHostMalloc'd memory into every GPU's
+// address space), so a kernel can write a small result straight into it.
+extern "C" int bm_host_writable(const void *p, size_t bytes, int *ok) {
+  if (!ok) {
+    bm_set_error("bm_host_writable: null result pointer");
+    return BM_E_ARG;
+  }
+  *ok = 0;
+  if (!p || bytes == 0) return BM_OK;
+  const char *lo = static_cast<const char *>(p);
+  for (const char *q : {lo, lo + bytes - 1}) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();  // unknown (pageable) memory: not writable, not an error
+      return BM_OK;
+    }
+    if (a.type != hipMemoryTypeHost || a.devicePointer != (void *)q) return BM_OK;
+  }
+  *ok = 1;
+  return BM_OK;
+}

@@ -23,6 +23,7 @@ SIGNATURES = {
     "bm_abi_version": (_c.c_int, []),
     "bm_last_error": (_c.c_char_p, []),
     "bm_device_cus": (_c.c_int, []),
+    "bm_host_writable": (_c.c_int, [_c.c_void_p, _c.c_size_t, _c.POINTER(_c.c_int)]),
     "bm_copy_strided": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _i64p, _i64p, _i64p,
                                    _c.c_int, _c.c_void_p]),
     "bm_permute": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _i64p,

@@ -97,6 +97,13 @@ class HipBackend(object):
     def _ptr(t, off=0):
         return ctypes.c_void_p(t.data_ptr() + int(off))
 
+    def host_writable(self, t):
+        """True if kernels can store into host tensor ``t`` at its own address."""
+        ok = ctypes.c_int(0)
+        _lib.check(self.lib.bm_host_writable(self._ptr(t), t.numel() * t.element_size(), ctypes.byref(ok)),
+                   "bm_host_writable")
+        return bool(ok.value)
+
     def copy_strided(self, src, src_off, dst, dst_off, shape, sstrides, dstrides, es):
         """dst[dst_off + idx . dstrides] = src[src_off + idx . sstrides] (offsets in bytes)."""
         nd = len(shape)

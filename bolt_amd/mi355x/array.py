@@ -25,7 +25,7 @@ from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
 from bolt_amd.mi355x.context import local_shape
 from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, permute_sharded, redistribute_rows, select_sharded, _empty
-from bolt_amd.mi355x.transfer import to_device, to_host
+from bolt_amd.mi355x.transfer import finish_host_result, host_result, to_device, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
 from bolt_amd.utils import tupleize, argpack, inshape, istransposeable
@@ -580,6 +580,11 @@ class BoltArrayMI355X(BoltArray):
             # every output lives on this rank (or this rank's slab of them)
             loc_out = tuple(lshape[i] for i in kept)
             nout = int(np.prod(loc_out, dtype=np.int64))
+            host = host_result(be, nout * out_dtype.itemsize, dev) if ctx.world_size == 1 and nloc else None
+            if host is not None:
+                # the kernel stores the result into page-locked host memory
+                be.reduce(stat, src, code, O, R, I, host, ocode)
+                return finish_host_result(host, dev, out_dtype, out_shape), out_dtype
             out = _empty(nout * out_dtype.itemsize, dev)
             if nout and nloc:
                 be.reduce(stat, src, code, O, R, I, out, ocode)

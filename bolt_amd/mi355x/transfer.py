@@ -24,6 +24,10 @@ SMALL = 8 << 20           # below this: one pinned buffer, no pipeline
 THREADS = int(os.environ.get("BOLT_AMD_COPY_THREADS", "8"))        # host memcpy threads per chunk
 H2D_DIRECT = os.environ.get("BOLT_AMD_H2D", "direct") == "direct"  # the runtime's pageable copy
 
+# statistics results up to SMALL bytes are stored by the reduction kernel
+# straight into a page-locked host buffer (no D2H copy launch)
+ZERO_COPY = os.environ.get("BOLT_AMD_ZERO_COPY", "1") != "0"
+
 _POOL = None
 
 
@@ -113,3 +117,24 @@ def to_host(t, dtype, shape):
     evs[(len(starts) - 1) % 2].synchronize()
     _par_copy(out[lo:n], bufs[(len(starts) - 1) % 2].numpy()[:n - lo])
     return out.view(dtype).reshape(shape)
+
+
+def host_result(backend, nbytes, device):
+    """A page-locked host buffer of ``nbytes`` that kernels on ``device`` can
+    store into, or None (zero-copy results off, not a GPU, too large, or the
+    allocation is not device-addressable)."""
+    if not ZERO_COPY or device.type != "cuda" or not 0 < nbytes <= SMALL:
+        return None
+    writable = getattr(backend, "host_writable", None)
+    if writable is None:
+        return None
+    import torch
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    return host if writable(host) else None
+
+
+def finish_host_result(host, device, dtype, shape):
+    """Wait for the kernel that fills ``host`` and view it as the result."""
+    import torch
+    torch.cuda.current_stream(device).synchronize()
+    return host.numpy().view(np.dtype(dtype)).reshape(shape)

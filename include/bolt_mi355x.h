@@ -70,6 +70,16 @@ const char *bm_last_error(void);
 int bm_device_cus(void);
 
 /*
+ * bm_host_writable -- *ok = 1 if [p, p + bytes) is page-locked host memory that
+ * the current device addresses at the same pointer, else 0.  Statistics with
+ * small results (mean/var/std/sum over most axes, array.py:284-395) pass such
+ * a buffer as bm_reduce's `out`: the kernel stores the result into host
+ * memory and the separate device-to-host copy (collect, array.py:1012-1014)
+ * disappears.
+ */
+int bm_host_writable(const void *p, size_t bytes, int *ok);
+
+/*
  * bm_copy_strided -- dst[i] = src[i] over an N-d index space.
  *
  * The single data-movement primitive of the backend.  It replaces every

@@ -67,6 +67,9 @@ def test_argument_errors(lib):
     assert lib.bm_record_gather(None, None, 1, 8, 8, None, 2, _lib.i64_array([0, 4, 0, 4, 4, 8, 4, 9]), 8,
                                 None) == -1
     assert lib.bm_record_gather(None, None, 1, 8, 8, None, 9, None, 8, None) == -1
+    ok = ctypes.c_int(7)
+    assert lib.bm_host_writable(None, 0, None) == -1
+    assert lib.bm_host_writable(None, 16, ctypes.byref(ok)) == 0 and ok.value == 0
 
 
 def test_workspace_and_state_sizes(lib):

@@ -258,3 +258,33 @@ def test_reduce_beyond_one_launch(O, R, I):
     assert torch.equal(out.view(torch.float32), want)  # small integers: exact in float64, one rounding
     del x, src, out, want
     torch.cuda.empty_cache()
+
+
+def test_host_writable_and_zero_copy_statistics(monkeypatch):
+    """Small statistics are stored by the kernel into page-locked host memory
+    (bm_host_writable); the result equals the device-buffer + copy path."""
+    import torch
+    import bolt_amd as bolt
+    from bolt_amd import MI355XContext
+    from bolt_amd.mi355x import transfer
+    from bolt_amd.mi355x._ops import backend_for
+    dev = torch.device("cuda", 0)
+    be = backend_for(dev)
+    assert be.host_writable(torch.empty(4096, dtype=torch.uint8, pin_memory=True))
+    assert not be.host_writable(torch.empty(4096, dtype=torch.uint8, device=dev))
+    assert not be.host_writable(torch.empty(4096, dtype=torch.uint8))  # pageable
+    ctx = MI355XContext(device="cuda:0")
+    rng = np.random.default_rng(3)
+    x = (1000 + 50 * rng.standard_normal((300, 64, 48))).astype(np.float32)
+    u = rng.integers(0, 65536, size=(40, 33, 17)).astype(np.uint16)
+    b, bu = bolt.array(x, ctx), bolt.array(u, ctx)
+    s = b.swap((0,), (0, 1))
+    cases = [(s, "mean", 2), (s, "std", 2), (b, "mean", 0), (b, "var", (0, 2)), (bu, "var", 0),
+             (bu, "sum", 0), (bu, "max", (1, 2)), (b, "std", None)]
+    got = {}
+    for zc in (True, False):
+        monkeypatch.setattr(transfer, "ZERO_COPY", zc)
+        got[zc] = [getattr(a, name)(axis=ax) for a, name, ax in cases]
+    for (a, name, ax), z, d in zip(cases, got[True], got[False]):
+        z, d = np.asarray(z), np.asarray(d)
+        assert z.shape == d.shape and z.dtype == d.dtype and z.tobytes() == d.tobytes(), (name, ax)
