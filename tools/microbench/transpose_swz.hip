@@ -59,6 +59,55 @@ __global__ void __launch_bounds__(THREADS) k_pad(const uint32_t* __restrict__ sr
   }
 }
 
+// cache policy variants of the padded kernel: NTL / NTS = non-temporal loads / stores
+template <int TA, int TB, int THREADS, bool NTL, bool NTS>
+__global__ void __launch_bounds__(THREADS) k_pol(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                 int64_t La, int64_t Lb, int64_t ntB) {
+  constexpr int VEC = 4;
+  __shared__ uint32_t tile[TB][TA + 1];
+  constexpr int NVA = TA / VEC, RPA = THREADS / NVA, NL = TB / RPA;
+  constexpr int NVB = TB / VEC, RPB = THREADS / NVB, NS = TA / RPB;
+  const int tx = threadIdx.x % NVA, ty = threadIdx.x / NVA;
+  const int ux = threadIdx.x % NVB, uy = threadIdx.x / NVB;
+  const int64_t t = blockIdx.x;
+  const int64_t tb = t % ntB, ta = t / ntB;
+  const int64_t a0 = ta * TA, b0 = tb * TB;
+  u4 v[NL];
+#pragma unroll
+  for (int it = 0; it < NL; ++it) {
+    const int rb = ty + it * RPA;
+    const u4* p = reinterpret_cast<const u4*>(src + (b0 + rb) * La + a0 + tx * VEC);
+    if (b0 + rb < Lb) v[it] = NTL ? __builtin_nontemporal_load(p) : *p;
+  }
+#pragma unroll
+  for (int it = 0; it < NL; ++it) {
+    const int rb = ty + it * RPA;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) tile[rb][tx * VEC + k] = v[it][k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NS; ++it) {
+    const int ra = uy + it * RPB;
+    if (b0 + ux * VEC + VEC - 1 < Lb) {
+      u4 w;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) w[k] = tile[ux * VEC + k][ra];
+      u4* q = reinterpret_cast<u4*>(dst + (a0 + ra) * Lb + b0 + ux * VEC);
+      if (NTS) __builtin_nontemporal_store(w, q); else *q = w;
+    } else {
+      for (int k = 0; k < VEC; ++k)
+        if (b0 + ux * VEC + k < Lb) dst[(a0 + ra) * Lb + b0 + ux * VEC + k] = tile[ux * VEC + k][ra];
+    }
+  }
+}
+
+template <int TA, int TB, int THREADS, bool NTL, bool NTS>
+void launch_pol(const void* src, void* dst, int64_t La, int64_t Lb) {
+  const int64_t ntB = (Lb + TB - 1) / TB, ntiles = (La / TA) * ntB;
+  k_pol<TA, TB, THREADS, NTL, NTS><<<(int)ntiles, THREADS>>>((const uint32_t*)src, (uint32_t*)dst, La, Lb, ntB);
+}
+
 // TA = 64 words (16 chunks of 16 B per row), TB = 4 * 64 rows per reading wave
 // pass: lanes along b, 4 rows each.
 template <int TA, int TB, int THREADS>
@@ -140,15 +189,11 @@ int main() {
     for (int64_t a = 0; a < La; ++a) ref[a * Lb + b] = h[b * La + a];
   CK(hipMemcpy(src, h.data(), nbytes, hipMemcpyHostToDevice));
   std::vector<Variant> vs = {
-      {"pad 64x256 t256", &launch_v<64, 256, 256, false>, {}, false},
-      {"pad 64x256 +16K (2/CU)", &launch_v<64, 256, 256, false, 16>, {}, false},
-      {"pad 64x256 +40K (1/CU)", &launch_v<64, 256, 256, false, 40>, {}, false},
-      {"swz 64x256 t256", &launch_v<64, 256, 256, true>, {}, false},
-      {"pad 64x128 t256", &launch_v<64, 128, 256, false>, {}, false},
-      {"pad 64x128 +32K (2/CU)", &launch_v<64, 128, 256, false, 32>, {}, false},
-      {"pad 64x128 +12K (3/CU)", &launch_v<64, 128, 256, false, 12>, {}, false},
       {"pad 32x256 t256", &launch_v<32, 256, 256, false>, {}, false},
-      {"pad 32x256 +32K (2/CU)", &launch_v<32, 256, 256, false, 32>, {}, false},
+      {"pad 64x128 t256", &launch_v<64, 128, 256, false>, {}, false},
+      {"pad 64x256 t256", &launch_v<64, 256, 256, false>, {}, false},
+      {"pad 32x256 t256 (again)", &launch_v<32, 256, 256, false>, {}, false},
+      {"pad 64x128 t256 (again)", &launch_v<64, 128, 256, false>, {}, false},
   };
   for (auto& v : vs) {
     CK(hipMemset(dst, 0, nbytes));
