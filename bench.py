@@ -31,6 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_GBPS = 6290.0      # measured float4 copy on MI355X (MI355X_MICROARCH.md), SURVEY 8(d)
 XGMI_LINK_GBPS = 153.0      # per link, per direction
 
 CONFIGS = {
@@ -371,6 +372,8 @@ def main():
                         "peak": peak, "unit": "GB/s per rank (egress)",
                         "frac": round(payload / (a2a / 1e3) / 1e9 / peak, 4) if a2a else None,
                         "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
+    line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
+    line["roofline"]["measured_copy_peak"] = HBM_COPY_GBPS
     if rank == 0 and world == 1 and not args.no_pmc:
         traffic, note = pmc_traffic(args.config)
         line["roofline"]["traffic"] = int(traffic) if traffic else None

@@ -92,11 +92,10 @@ int main() {
   for (int64_t i = 0; i < nbytes; ++i) h[i] = (uint8_t)((i * 2654435761ull) >> 13);
   CK(hipMemcpy(src, h.data(), nbytes, hipMemcpyHostToDevice));
   std::vector<Variant> vs = {
-      V<uint32_t, 64, 256, 256>(),  V<uint32_t, 64, 256, 512>(),  V<uint32_t, 128, 256, 1024>(),
-      V<uint32_t, 128, 128, 512>(), V<uint32_t, 256, 128, 1024>(), V<uint32_t, 64, 512, 1024>(),
-      V<uint32_t, 128, 128, 256>(), V<uint32_t, 32, 256, 256>(),
-      V<uint64_t, 32, 256, 256>(),  V<uint64_t, 64, 128, 512>(),  V<uint64_t, 64, 256, 1024>(),
-      V<uint16_t, 128, 256, 256>(), V<uint16_t, 128, 256, 512>(), V<uint16_t, 256, 256, 1024>(),
+      V<uint32_t, 64, 256, 256>(),
+      V<uint16_t, 128, 256, 256>(), V<uint16_t, 128, 512, 1024>(), V<uint16_t, 128, 512, 512>(),
+      V<uint8_t, 128, 256, 256>(),  V<uint8_t, 256, 512, 1024>(),  V<uint8_t, 128, 512, 512>(),
+      V<uint8_t, 256, 256, 512>(),
   };
   int cur_es = 0;
   for (auto& v : vs) {
