@@ -65,7 +65,9 @@ def getplan(vshape, dtype, size="150", axes=None, padding=None):
             remsize = 1.0 * nelements * elsize
             s = []
             for (i, d) in enumerate(dims):
-                minsize = remsize / d
+                # a zero-length axis gives nan / inf as in the reference (no warning)
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    minsize = remsize / d
                 if minsize >= size:
                     s.append(1)
                     remsize = minsize
