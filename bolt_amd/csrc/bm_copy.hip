@@ -44,12 +44,18 @@ constexpr int kThreads = 256;
 #define BM_PK 1  // packed-word tiles for 1-/2-byte transposes (A/B knob)
 #endif
 #ifndef BM_PK16_TA  // packed tiles, profiles/r01_ab_pk2.log: u16 128x256 +9%, u8 128x256 +11% over
-#define BM_PK16_TA 128  // element-wise LDS tiles (64x512 / 128x512 / 256x256 measured and lose)
-#define BM_PK16_TB 256
+#define BM_PK16_TA 128  // element-wise LDS tiles; u16 128x512 with 1024 threads (128 KiB of LDS,
+#define BM_PK16_TB 512  // 256-B source x 1-KiB destination segments) +6-8% more (r01_ab_pk3.log)
+#endif
+#ifndef BM_PK16_NT
+#define BM_PK16_NT 1024
 #endif
 #ifndef BM_PK8_TA
 #define BM_PK8_TA 128
-#define BM_PK8_TB 256
+#define BM_PK8_TB 512
+#endif
+#ifndef BM_PK8_NT
+#define BM_PK8_NT 1024
 #endif
 #ifndef BM_RC_XCD
 #define BM_RC_XCD 0  // XCD-grouped covering grid: +5% in a C4 microbench (r01_rc1) but -3..-20% in the product A/B (r01_ab_rc)
@@ -241,17 +247,17 @@ __global__ void __launch_bounds__(kThreads)
 // Requires 16-B aligned source and destination rows (the caller checks).
 // (tile sweep: element-wise LDS tiles move u16 / u8 at 4.6 / 3.0 TB/s,
 // profiles/r01_tt2.log)
-template <typename T, int TA, int TB>
-__global__ void __launch_bounds__(kThreads)
+template <typename T, int TA, int TB, int NT = kThreads>
+__global__ void __launch_bounds__(NT)
     k_transpose_pk(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
   constexpr int P = 4 / (int)sizeof(T);  // rows per word
   constexpr int VA = 16 / (int)sizeof(T);
   constexpr int TBW = TB / P;            // word rows in the tile
   constexpr int NVA = TA / VA;           // lanes per word row (load)
-  constexpr int RGA = kThreads / NVA;    // word rows per pass
+  constexpr int RGA = NT / NVA;    // word rows per pass
   constexpr int NL = TBW / RGA;
   constexpr int NVB = TBW / 4;           // lanes per destination row (4 words each)
-  constexpr int RPB = kThreads / NVB;
+  constexpr int RPB = NT / NVB;
   constexpr int NS = TA / RPB;
   constexpr int BITS = 8 * (int)sizeof(T);
   static_assert(NL >= 1 && TBW % RGA == 0 && NS >= 1 && TA % RPB == 0, "tile too small for the thread layout");
@@ -651,10 +657,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     uint64_t g = tp.ntiles;
     if (g > kMaxGrid) g = kMaxGrid;
     if (es == 2)
-      k_transpose_pk<uint16_t, BM_PK16_TA, BM_PK16_TB><<<(int)g, kThreads, 0, st>>>((const uint16_t *)src,
+      k_transpose_pk<uint16_t, BM_PK16_TA, BM_PK16_TB, BM_PK16_NT><<<(int)g, BM_PK16_NT, 0, st>>>((const uint16_t *)src,
                                                                                  (uint16_t *)dst, tp);
     else
-      k_transpose_pk<uint8_t, BM_PK8_TA, BM_PK8_TB><<<(int)g, kThreads, 0, st>>>((const uint8_t *)src,
+      k_transpose_pk<uint8_t, BM_PK8_TA, BM_PK8_TB, BM_PK8_NT><<<(int)g, BM_PK8_NT, 0, st>>>((const uint8_t *)src,
                                                                               (uint8_t *)dst, tp);
     return BM_OK;
   }
