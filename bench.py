@@ -176,11 +176,54 @@ def steps_of(cfg, b, world=1):
     raise ValueError(cfg)
 
 
+# leading-axis rows of the per-GPU shard timed by local_numpy_baseline (~0.5-1 GB)
+LOCAL_SAMPLE_ROWS = {"C3": 64, "C4": 256, "C5": 8, "target64": 64}
+
+
+def local_numpy_baseline(cfg, shape, dtype):
+    """The reference local mode's numpy calls (bolt/local/array.py) for the
+    config's permute and statistic ops, one host thread, on a slab of the
+    leading axis; chunk/unchunk have no local-mode counterpart and are left out."""
+    rows = min(shape[0], LOCAL_SAMPLE_ROWS[cfg])
+    sample_shape = (rows,) + tuple(shape[1:])
+    rng = np.random.default_rng(0)
+    if np.dtype(dtype).kind == "u":
+        x = rng.integers(0, np.iinfo(dtype).max + 1, size=sample_shape, dtype=dtype)
+    else:
+        x = rng.standard_normal(sample_shape).astype(dtype)
+    nd = x.ndim
+    swap01 = (1, 0) + tuple(range(2, nd))
+    ops = {"C3": [("swap", lambda: np.ascontiguousarray(x.transpose(1, 2, 0, 3))),
+                  ("T", lambda: np.ascontiguousarray(x.T))],
+           "C4": [("swap", lambda: np.ascontiguousarray(x.transpose(swap01))),
+                  ("var", lambda: x.var(axis=0))],
+           "C5": [("T", lambda: np.ascontiguousarray(x.T)),
+                  ("transpose", lambda: np.ascontiguousarray(x.transpose(2, 0, 4, 1, 3)))],
+           "target64": [("swap", lambda: np.ascontiguousarray(x.transpose(1, 2, 0, 3))),
+                        ("mean", lambda: x.mean(axis=0)),
+                        ("std", lambda: x.std(axis=0))]}[cfg]
+    N = x.nbytes
+    total, parts = 0, []
+    t0 = time.perf_counter()
+    for name, f in ops:
+        u = time.perf_counter()
+        r = f()
+        parts.append("%s %.2fs" % (name, time.perf_counter() - u))
+        total += 2 * N if r.shape == x.shape[::-1] or r.size == x.size else N + r.nbytes
+        del r
+    el = time.perf_counter() - t0
+    return {"value": total / el / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "the reference local mode's numpy calls on %s %s (a leading-axis slab of the "
+                      "shard; chunk/unchunk not included): %s" % (np.dtype(dtype).name, str(sample_shape),
+                                                                   " + ".join(parts)),
+            "host_cpus": os.cpu_count()}
+
+
 def cpu_baseline(cfg, shape, dtype, rows):
     """Oracle (record-level restatement of the reference Spark path), 1 core, bounded sample."""
     from oracle import bolt_oracle as O
     if cfg != "C2":
-        return None
+        return local_numpy_baseline(cfg, shape, dtype)
     rng = np.random.default_rng(0)
     sample_shape = (rows,) + tuple(shape[1:])
     x = (1000 + 50 * rng.standard_normal(sample_shape)).astype(dtype)
@@ -271,16 +314,23 @@ def main():
     from bolt_amd.mi355x._ops import backend_for
     be = backend_for(dev)
     kev = []
+    # event pairs made before the timed region (one permute launch per swap on
+    # one GPU; the pipelined multi-GPU swap launches more and draws extra pairs)
+    kpool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(args.steps)]
     permute0 = be.permute
     timing = {"on": False}
 
     def timed_permute(*a, **k):
         if not timing["on"]:
             return permute0(*a, **k)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(torch.cuda.current_stream(dev))
+        if len(kev) < len(kpool):
+            e0, e1 = kpool[len(kev)]
+        else:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         permute0(*a, **k)
-        e1.record(torch.cuda.current_stream(dev))
+        e1.record(stream)
         kev.append((e0, e1))
     be.permute = timed_permute
     from bolt_amd.mi355x import dist as bdist
