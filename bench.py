@@ -341,12 +341,14 @@ def main():
     for i in range(args.steps):
         for k, (_, call, _) in enumerate(ops):
             if k == 0:
-                ev[i][0].record(stream)
+                if world > 1:
+                    ev[i][0].record(stream)
                 timing["on"] = True
             r = call()
             if k == 0:
                 timing["on"] = False
-                ev[i][1].record(stream)
+                if world > 1:
+                    ev[i][1].record(stream)
             del r
     barrier()
     elapsed = time.perf_counter() - t0
@@ -361,8 +363,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    swap_ms = float(np.mean([a.elapsed_time(z) for a, z in ev]))   # the whole swap call
-    kern_ms = float(np.mean([a.elapsed_time(z) for a, z in kev])) if kev else swap_ms
+    # On one GPU the swap call is the one permute launch, so only the kernel's
+    # own event pair is recorded (each extra stream event adds a few us between
+    # the kernels); across GPUs the call's pair brackets the whole exchange.
+    kern_ms = float(np.mean([a.elapsed_time(z) for a, z in kev])) if kev else None
+    swap_ms = float(np.mean([a.elapsed_time(z) for a, z in ev])) if world > 1 else kern_ms
+    if kern_ms is None:  # (no permute launch in the op: the step's wall time bounds it)
+        kern_ms = swap_ms if swap_ms is not None else elapsed / args.steps * 1e3
+        swap_ms = kern_ms
     per = {name: nb * world for name, _, nb in ops}
     total = sum(per.values()) * args.steps
     value = total / elapsed / 1e9
