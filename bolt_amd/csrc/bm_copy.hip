@@ -60,6 +60,9 @@ constexpr int kThreads = 256;
 #ifndef BM_RC_XCD
 #define BM_RC_XCD 0  // XCD-grouped covering grid: +5% in a C4 microbench (r01_rc1) but -3..-20% in the product A/B (r01_ab_rc)
 #endif
+#ifndef BM_RC_SRC_MAXB
+#define BM_RC_SRC_MAXB 0  // rows up to this many bytes are walked in source order (A/B knob)
+#endif
 #ifndef BM_GEN_GRIDCAP
 #define BM_GEN_GRIDCAP 4096  // generic copies: grid-stride (uncapped measured -20% on reversed slices, r01_index2)
 #endif
@@ -461,6 +464,13 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     for (const Dim &x : outer)
       if ((x.ss * es) % VB || (x.ds * es) % VB) ok = false;
     if (ok) break;
+  }
+  if (row_bytes <= BM_RC_SRC_MAXB) {
+    // walk the rows in source order: reads stream, short rows scatter on the
+    // store side (any order of the outer dims covers the same index space)
+    std::stable_sort(outer.begin(), outer.end(), [](const Dim &x, const Dim &y) {
+      return std::llabs(x.ss) > std::llabs(y.ss);
+    });
   }
   Decomp d;
   if (!fill_decomp(d, outer)) {

@@ -7,6 +7,8 @@
 //         writes 1 KiB contiguous (the product's order);
 //   src   source order: a wave reads 1 KiB contiguous and writes 8 rows at
 //         512-KiB destination stride;
+//   dstwW destination order within c-windows of W rows (W source pages in
+//         flight instead of C);
 //   tileN 2-D tiles of 8 b x N c rows per wave: each load instruction reads
 //         1 KiB contiguous (8 b of one c), the N loads of a lane cover N
 //         consecutive c, so each destination row (a, b) receives an N*128-B
@@ -79,6 +81,31 @@ __global__ void __launch_bounds__(256) k_tile(const u4* __restrict__ src, u4* __
   for (int u = 0; u < N; ++u) __builtin_nontemporal_store(r[u], dst + ((a * B + b) * C + c0 + u) * 8 + v);
 }
 
+// destination order inside c-windows of W: for each a, for each window, the
+// rows (b, c) with c in the window, c fastest -- a window touches W source
+// pages (one per c) instead of all C.
+template <int U, int W>
+__global__ void __launch_bounds__(256) k_dstw(const u4* __restrict__ src, u4* __restrict__ dst) {
+  const uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x;
+  u4 r[U];
+  uint64_t dof[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t g = base + (uint64_t)u * 256;
+    const uint64_t row = g >> 3, v = g & 7;       // traversal index (a, cw, b, ci)
+    const uint64_t ci = row % W;
+    const uint64_t t1 = row / W;
+    const uint64_t b = t1 % B;
+    const uint64_t t2 = t1 / B;
+    const uint64_t cw = t2 % (C / W), a = t2 / (C / W);
+    const uint64_t c = cw * W + ci;
+    r[u] = __builtin_nontemporal_load(src + ((c * A + a) * B + b) * 8 + v);
+    dof[u] = ((a * B + b) * C + c) * 8 + v;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) __builtin_nontemporal_store(r[u], dst + dof[u]);
+}
+
 static bool check(const u4* dsrc, const u4* ddst) {
   for (int t = 0; t < 64; ++t) {
     const uint64_t c = (t * 977) % C, a = (t * 131) % A, b = (t * 37 + 5) % B;
@@ -130,5 +157,10 @@ int main() {
   run("tile16", [&] { k_tile<16><<<(B / 32) * (C / 16) * A, 256>>>(src, dst); }, src, dst);
   run("dst", [&] { k_dst<U><<<g4, 256>>>(src, dst); }, src, dst);
   run("src", [&] { k_src<U><<<g4, 256>>>(src, dst); }, src, dst);
+  run("dstw64", [&] { k_dstw<U, 64><<<g4, 256>>>(src, dst); }, src, dst);
+  run("dstw256", [&] { k_dstw<U, 256><<<g4, 256>>>(src, dst); }, src, dst);
+  run("dstw1024", [&] { k_dstw<U, 1024><<<g4, 256>>>(src, dst); }, src, dst);
+  run("dst", [&] { k_dst<U><<<g4, 256>>>(src, dst); }, src, dst);
+  run("dstw256", [&] { k_dstw<U, 256><<<g4, 256>>>(src, dst); }, src, dst);
   return 0;
 }
