@@ -122,3 +122,17 @@ def test_bench_steps_weak_scaling(world):
             p.kill()
     assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("cfg,shape,dtype", [
+    ("C3", (4, 8, 8, 32), np.float32), ("C4", (6, 16, 16), np.uint16),
+    ("C5", (2, 4, 4, 4, 4), np.float64), ("target64", (4, 8, 8, 32), np.float32)])
+def test_local_numpy_baseline_fields(cfg, shape, dtype, monkeypatch):
+    """bench.py's CPU baseline for the non-default configs: the reference local
+    mode's numpy calls on a leading-axis slab, one thread, reported as GB/s."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.setitem(bench.LOCAL_SAMPLE_ROWS, cfg, 2)
+    r = bench.cpu_baseline(cfg, shape, dtype, rows=None)
+    assert r["unit"] == "GB/s" and r["cores"] == 1 and r["kind"] == "port"
+    assert r["value"] > 0 and "(2," in r["sample"]
