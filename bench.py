@@ -392,7 +392,7 @@ def main():
         "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
         "config": {"workload": desc, "global_shape": list(gshape), "split": split,
                    "parallelism": "dp%d (records sharded on the leading key axis)" % world,
-                   "collectives": "RCCL (torch.distributed nccl)" if backend == "nccl" or world == 1
+                   "collectives": "RCCL via libbolt_mi355x (bm_alltoallv / bm_allgatherv)" if backend == "nccl" or world == 1
                                   else "%s, host-staged (one-GPU rehearsal, not a measurement)" % backend,
                    "bytes_per_step": {k: int(v) for k, v in per.items()}},
         "roofline": {
@@ -422,7 +422,7 @@ def main():
             line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
         a2a = phases.get("exchange")
         peak = (G - 1) * XGMI_LINK_GBPS
-        line["xgmi"] = {"op": "RCCL all_to_all_single inside the pipelined swap exchange "
+        line["xgmi"] = {"op": "RCCL send/recv group (bm_alltoallv) inside the pipelined swap exchange "
                               "(achieved = peer payload / whole exchange time: a lower bound)",
                         "payload_bytes_per_rank": int(payload),
                         "avg_ms": round(a2a, 4) if a2a else None,
@@ -442,6 +442,8 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        barrier()
+        ctx.close()  # the library's RCCL communicator, before the process group
         dist.destroy_process_group()
 
 

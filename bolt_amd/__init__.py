@@ -12,7 +12,7 @@ ChunkedArray chunk/unchunk/keys_to_values/values_to_keys, swap, transpose,
 sum/mean/var/std.  Multi-GPU: one process per GPU, records sharded along the
 leading key axis, RCCL all-to-all for swaps and all_gather for statistics.
 """
-from bolt_amd.factory import array, ones, zeros  # noqa: F401
+from bolt_amd.factory import array, ones, zeros, concatenate  # noqa: F401
 from bolt_amd.mi355x.context import MI355XContext  # noqa: F401
 from bolt_amd.mi355x.construct import ConstructMI355X  # noqa: F401
 

@@ -13,10 +13,18 @@
 //   Long R is split into chunks over blocks (enough waves to fill 256 CUs);
 //   chunk states go to a workspace and a combine kernel merges them in chunk
 //   order (deterministic) and finalises.
-// Numerics: float64 pivot-shifted sums per lane (pivot = the lane's first
-// element: S1 = sum(x-K), S2 = sum((x-K)^2), mean = K + S1/n,
-// M2 = S2 - S1^2/n), Chan combination everywhere else.  SUM over integers is
-// a uint64 modular sum truncated to the input width; SUM over bool is OR.
+// Numerics (all float64):
+//   var / std: batched Welford.  Each lane reduces the B values of one load
+//     batch (B = vectors in flight x vector width, 1..32) around a pivot that
+//     is one of those values, so the batch's M2 = S2 - S1^2/B carries at most
+//     O(B eps) relative error whatever the data's offset or outliers; the
+//     batch state (B, mean_b, M2_b) is then merged into the lane's running
+//     (n, mean, M2) by Chan's formula (statcounter.py:85-96), as are lanes,
+//     row phases, chunks and ranks, always in a fixed order (deterministic).
+//   mean: pivot-shifted sums around the (row, chunk)'s first element,
+//     mean = K + S1/n (no cancellation: the error is eps-relative to max|x|).
+//   SUM over floats is a float64 sum; over integers a uint64 modular sum
+//   truncated to the input width; over bool an OR.
 // All are HBM-bound: algorithmic bytes = N*elem_bytes + nout*out_bytes.
 #include "bm_common.h"
 #include "../../include/bolt_mi355x.h"
@@ -39,12 +47,28 @@ constexpr int kColsUnroll = BM_COLS_UNROLL;
 #endif
 constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
 
-enum Mode { M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4, M_MAX = 5, M_MIN = 6 };
+enum Mode {
+  M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4, M_MAX = 5, M_MIN = 6,
+  M_FPROD = 7, M_IPROD = 8, M_LAND = 9, M_BAND = 10, M_BOR = 11, M_BXOR = 12, M_FMAX = 13, M_FMIN = 14
+};
 
-// "bit modes" keep a uint64 accumulator: modular integer sum, OR (bool sum),
-// and max / min holding the element's own bits (typed compares below).
+// "bit modes" keep a uint64 accumulator: modular integer sum / product,
+// logical OR (bool sum, logical_or) / AND, bitwise and / or / xor, and
+// max / min / fmax / fmin holding the element's own bits (typed compares).
 template <int MODE> constexpr bool bit_mode() {
-  return MODE == M_ISUM || MODE == M_OR || MODE == M_MAX || MODE == M_MIN;
+  return MODE == M_ISUM || MODE == M_OR || MODE == M_MAX || MODE == M_MIN || MODE == M_IPROD ||
+         MODE == M_LAND || MODE == M_BAND || MODE == M_BOR || MODE == M_BXOR || MODE == M_FMAX ||
+         MODE == M_FMIN;
+}
+// float-accumulating modes: a float64 sum or product
+template <int MODE> constexpr bool facc_mode() { return MODE == M_FSUM || MODE == M_FPROD; }
+template <int MODE> __device__ __forceinline__ double fident() { return MODE == M_FPROD ? 1.0 : 0.0; }
+template <int MODE> __device__ __forceinline__ double fop(double a, double b) {
+  return MODE == M_FPROD ? a * b : a + b;
+}
+// modes meaningless for floating inputs (numpy raises for bitwise ufuncs)
+template <int MODE> constexpr bool int_only_mode() {
+  return MODE == M_ISUM || MODE == M_IPROD || MODE == M_BAND || MODE == M_BOR || MODE == M_BXOR;
 }
 
 template <typename T> __device__ __forceinline__ double to_f64(T x) { return (double)x; }
@@ -76,6 +100,19 @@ template <typename T, bool MAX> __device__ __forceinline__ T pick(T a, T b) {
   if (is_nan(b)) return b;
   return MAX ? (b > a ? b : a) : (b < a ? b : a);
 }
+// numpy.fmax / numpy.fmin: a NaN operand loses (NaN only if both are NaN)
+template <typename T, bool MAX> __device__ __forceinline__ T pickf(T a, T b) {
+  if (is_nan(a)) return b;
+  if (is_nan(b)) return a;
+  return MAX ? (b > a ? b : a) : (b < a ? b : a);
+}
+template <typename T> __device__ __forceinline__ T qnan() { return T(0); }
+template <> __device__ __forceinline__ _Float16 qnan<_Float16>() { return (_Float16)__builtin_nanf(""); }
+template <> __device__ __forceinline__ float qnan<float>() { return __builtin_nanf(""); }
+template <> __device__ __forceinline__ double qnan<double>() { return __builtin_nan(""); }
+template <typename T> constexpr bool is_float_t() {
+  return std::is_same<T, _Float16>::value || std::is_same<T, float>::value || std::is_same<T, double>::value;
+}
 
 template <typename T> struct Lim;
 template <> struct Lim<uint8_t> { static __device__ uint8_t lo() { return 0; } static __device__ uint8_t hi() { return 0xff; } };
@@ -94,16 +131,26 @@ template <> struct Lim<double> { static __device__ double lo() { return -__built
 template <typename T, int MODE> __device__ __forceinline__ uint64_t bident() {
   if (MODE == M_MAX) return bits_of<T>(Lim<T>::lo());
   if (MODE == M_MIN) return bits_of<T>(Lim<T>::hi());
+  // fmax / fmin: NaN is the identity of floats (all-NaN -> NaN)
+  if (MODE == M_FMAX) return bits_of<T>(is_float_t<T>() ? qnan<T>() : Lim<T>::lo());
+  if (MODE == M_FMIN) return bits_of<T>(is_float_t<T>() ? qnan<T>() : Lim<T>::hi());
+  if (MODE == M_IPROD || MODE == M_LAND) return 1;
+  if (MODE == M_BAND) return ~0ull;
   return 0;
 }
 template <typename T, int MODE> __device__ __forceinline__ uint64_t belem(T x) {
-  if (MODE == M_ISUM) return to_u64(x);
-  if (MODE == M_OR) return (uint64_t)(x != 0);
+  if (MODE == M_ISUM || MODE == M_IPROD) return to_u64(x);
+  if (MODE == M_OR || MODE == M_LAND) return (uint64_t)(x != 0);
   return bits_of<T>(x);
 }
 template <typename T, int MODE> __device__ __forceinline__ uint64_t bop(uint64_t a, uint64_t b) {
   if (MODE == M_ISUM) return a + b;
-  if (MODE == M_OR) return a | b;
+  if (MODE == M_IPROD) return a * b;  // modular: the low bits depend only on the low bits
+  if (MODE == M_OR || MODE == M_BOR) return a | b;
+  if (MODE == M_LAND || MODE == M_BAND) return a & b;
+  if (MODE == M_BXOR) return a ^ b;
+  if (MODE == M_FMAX || MODE == M_FMIN)
+    return bits_of<T>(pickf<T, MODE == M_FMAX>(from_bits<T>(a), from_bits<T>(b)));
   return bits_of<T>(pick<T, MODE == M_MAX>(from_bits<T>(a), from_bits<T>(b)));
 }
 
@@ -125,44 +172,96 @@ template <> struct Acc<M_MEAN> {
   __device__ double m2() const { return 0.0; }
 };
 
-template <> struct Acc<M_MOM> {
-  double K, S1, S2, S1b, S2b;
-  int64_t n;
-  __device__ void init() { K = 0; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 0; }
-  __device__ void first(double x) { K = x; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 1; }
-  __device__ void pivot(double k) { K = k; S1 = 0; S2 = 0; S1b = 0; S2b = 0; n = 0; }
-  __device__ double s1() const { return S1 + S1b; }
-  __device__ double s2() const { return S2 + S2b; }
-  __device__ void add(double x) {
-    const double dx = x - K;
-    S1 += dx;
-    S2 = fma(dx, dx, S2);
-    ++n;
+// (n, K, S1) of pivot-shifted sums -> mean
+__device__ __forceinline__ double mean_from_sums(double n, double K, double s1) {
+  return n > 0.0 ? K + s1 / n : 0.0;
+}
+
+// Batch moments of B values around the pivot K = x[0] (one of the values, so
+// S2 <= (1 + B) M2_b and the subtraction loses at most log2(B+1) bits),
+// returned in the frame shifted by the row's pivot P: mb = mean_b - P.
+// K - P is exact for values within a factor of two of P (offset data) and
+// otherwise rounds once, at the data's own scale.
+template <int B>
+__device__ __forceinline__ void batch_moments(const double (&x)[B], double P, double &mb, double &qb) {
+  const double K = x[0];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int i = 1; i < B; ++i) {
+    const double d = x[i] - K;
+    s1 += d;
+    s2 = fma(d, d, s2);
   }
-  __device__ void add2(double x, double y) {
-    const double dx = x - K, dy = y - K;
-    S1 += dx;
-    S2 = fma(dx, dx, S2);
-    S1b += dy;
-    S2b = fma(dy, dy, S2b);
-    n += 2;
+  constexpr double inv = 1.0 / (double)B;  // B is a power of two: exact
+  mb = fma(s1, inv, K - P);
+  const double q = fma(-s1, s1 * inv, s2);
+  qb = q > 0.0 ? q : 0.0;
+}
+
+// Chan merge of a batch (nb values, mean mb, M2 qb) into (mean, m2) holding
+// na values, with f = nb / (na + nb) and nf = na * f precomputed by the caller
+// (shared by the VEC columns of a lane).  na == 0 gives f = 1, nf = 0: the
+// batch is taken as is.
+__device__ __forceinline__ void merge_batch(double &mean, double &m2, double mb, double qb, double f,
+                                            double nf) {
+  const double delta = mb - mean;
+  mean = fma(delta, f, mean);
+  m2 = m2 + qb + delta * delta * nf;
+}
+
+__device__ __forceinline__ void batch_weights(double na, double nb, double &f, double &nf) {
+  if (na == nb) {
+    f = 0.5;  // equal halves (the butterfly and phase trees): no division
+  } else {
+    f = nb / (na + nb);
   }
-  __device__ double mean() const { return n ? K + (S1 + S1b) / (double)n : 0.0; }
-  __device__ double m2() const {
-    if (!n) return 0.0;
-    const double s1 = S1 + S1b;
-    const double v = (S2 + S2b) - s1 * (s1 / (double)n);
-    return v > 0.0 ? v : 0.0;
+  nf = na * f;
+}
+
+// 1/k for the k-th equal batch of a lane's main loop: f = B / ((k+1) B) =
+// 1/(k+1), the same correctly rounded value the division gives, from a table.
+constexpr int kInvN = 512;
+struct InvTab {
+  double v[kInvN];
+  constexpr InvTab() : v() {
+    for (int i = 1; i < kInvN; ++i) v[i] = 1.0 / (double)i;
   }
 };
+__device__ constexpr InvTab kInvTab{};
 
-// (n, K, S1, S2) of pivot-shifted sums -> mean, M2
-__device__ __forceinline__ void from_sums(double n, double K, double s1, double s2, double &mean,
-                                          double &m2) {
-  mean = n > 0.0 ? K + s1 / n : 0.0;
-  const double v = n > 0.0 ? s2 - s1 * (s1 / n) : 0.0;
-  m2 = v > 0.0 ? v : 0.0;
+__device__ __forceinline__ void uniform_weights(int64_t kb, double B, double &f, double &nf) {
+  f = kb + 1 < kInvN ? kInvTab.v[kb + 1] : 1.0 / (double)(kb + 1);
+  nf = ((double)kb * B) * f;
 }
+
+// Running Welford state of one output (rows kernel), in the frame shifted by
+// the row's pivot P.
+struct Wel {
+  double n, mean, m2;
+  int64_t kb;  // equal main-loop batches merged so far
+  __device__ void init() { n = 0.0; mean = 0.0; m2 = 0.0; kb = 0; }
+  template <int B> __device__ void add_main(const double (&x)[B], double P) {
+    double mb, qb, f, nf;
+    batch_moments<B>(x, P, mb, qb);
+    uniform_weights(kb, (double)B, f, nf);
+    merge_batch(mean, m2, mb, qb, f, nf);
+    ++kb;
+    n += (double)B;
+  }
+  template <int B> __device__ void add_batch(const double (&x)[B], double P) {
+    double mb, qb, f, nf;
+    batch_moments<B>(x, P, mb, qb);
+    batch_weights(n, (double)B, f, nf);
+    merge_batch(mean, m2, mb, qb, f, nf);
+    n += (double)B;
+  }
+  __device__ void add1(double y) {  // Welford's own update (statcounter.py:51-59), y = x - P
+    n += 1.0;
+    const double delta = y - mean;
+    mean += delta / n;
+    m2 = fma(delta, y - mean, m2);
+  }
+};
 
 // Chan et al. pairwise combination of (n, mean, M2) -- statcounter.py:85-96
 // in its exact form (no 10x heuristic needed in float64).
@@ -175,8 +274,14 @@ __device__ __forceinline__ void chan(double &na, double &ma, double &qa, double 
   }
   const double n = na + nb;
   const double delta = mb - ma;
-  ma = ma + delta * (nb / n);
-  if (need_m2) qa = qa + qb + delta * delta * (na * (nb / n));
+  double f;
+  if (na == nb) {
+    f = 0.5;
+  } else {
+    f = nb / n;
+  }
+  ma = fma(delta, f, ma);
+  if (need_m2) qa = qa + qb + delta * delta * (na * f);
   na = n;
 }
 
@@ -217,7 +322,25 @@ struct Sink {
   int final_out;
   double *p0;       // state plane 0 (mean / fsum) or uint64 plane (isum / or)
   double *p1;       // state plane 1 (M2)
+  double *p2;       // var / std chunk partials: the row's pivot P per output
+  int shifted;      // var / std: p0 holds mean - P (chunk partials in the workspace)
 };
+
+// var / std output of one (output, chunk): the Welford state is kept around
+// the pivot P (an element of the output's first row), mean_y = mean - P.
+// Final: var / std (M2 only); state: mean, M2 -- shifted for the workspace
+// partials (chunk 0 records P), absolute for bm_reduce_state.
+__device__ __forceinline__ void emit_mom(const Sink &sk, int64_t idx, int64_t e, int64_t c, double n,
+                                         double mean_y, double m2, double P) {
+  m2 = m2 > 0.0 ? m2 : 0.0;
+  if (sk.final_out) {
+    store_out(sk.out, idx, finish(sk.stat, 0.0, m2, n), sk.out_dtype);
+    return;
+  }
+  sk.p0[idx] = sk.shifted ? mean_y : P + mean_y;
+  sk.p1[idx] = m2;
+  if (sk.shifted && c == 0) sk.p2[e] = P;
+}
 
 template <int MODE>
 __device__ __forceinline__ void emit(const Sink &sk, int64_t e, double n, double mean, double m2,
@@ -225,7 +348,7 @@ __device__ __forceinline__ void emit(const Sink &sk, int64_t e, double n, double
   if (bit_mode<MODE>()) {
     if (sk.final_out) store_int(sk.out, e, u, sk.out_dtype);
     else ((uint64_t *)sk.p0)[e] = u;
-  } else if (MODE == M_FSUM) {
+  } else if (facc_mode<MODE>()) {
     if (sk.final_out) store_out(sk.out, e, mean, sk.out_dtype);
     else sk.p0[e] = mean;
   } else {
@@ -253,6 +376,7 @@ __global__ void __launch_bounds__(kThreads)
     k_red_cols(const T *__restrict__ src, ColsDesc d, Sink sk) {
   __shared__ double sm0[kThreads * VEC];
   __shared__ double sm1[(MODE == M_MOM) ? kThreads * VEC : 1];
+  __shared__ double smn[(MODE == M_MOM) ? kThreads : 1];
   const uint64_t ot = (uint64_t)d.tile0 + blockIdx.x;
   const uint64_t o = fd_div(ot, d.ntc);
   const uint64_t tc = ot - o * d.ntc.d;
@@ -265,16 +389,31 @@ __global__ void __launch_bounds__(kThreads)
   const bool active = col0 < d.I;
   const int64_t nph = d.nph;
 
-  Acc<(MODE == M_MOM) ? M_MOM : M_MEAN> acc[VEC];
+  Acc<M_MEAN> acc[VEC];
   double fs[VEC];
   uint64_t us[VEC];
+  // var / std: the lane's Welford state per column; the VEC columns share n
+  double wm[VEC], wq[VEC];
+  double wn = 0.0;
+  int64_t wkb = 0;  // equal main-loop batches merged
 #pragma unroll
-  for (int k = 0; k < VEC; ++k) { acc[k].init(); fs[k] = 0.0; us[k] = bident<T, MODE>(); }
+  for (int k = 0; k < VEC; ++k) {
+    acc[k].init(); fs[k] = fident<MODE>(); us[k] = bident<T, MODE>(); wm[k] = 0.0; wq[k] = 0.0;
+  }
 
+  double P[VEC];  // var / std: pivot per column, the column's element in row 0
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) P[k] = 0.0;
   if (active) {
     const T *base = src + ((int64_t)o * d.R) * d.I + col0;
     int64_t r = r_lo + ph;
-    if (MODE == M_MEAN || MODE == M_MOM) {
+    if (MODE == M_MOM) {
+      T p0v[VEC];
+      vload<T, VEC>(base, p0v);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) P[k] = to_f64(p0v[k]);
+    }
+    if (MODE == M_MEAN) {
       // one pivot per column for every row phase of the block (the chunk's
       // first row): the phases then combine by plain sums, no divisions
       T k0[VEC];
@@ -282,17 +421,34 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc[k].pivot(to_f64(k0[k]));
     }
-    if constexpr (MODE == M_MEAN || MODE == M_MOM || MODE == M_FSUM) {
+    if constexpr (MODE == M_MEAN || MODE == M_MOM || facc_mode<MODE>()) {
       // kColsUnroll rows in flight per lane; the adds stay in row order
       for (; r + (kColsUnroll - 1) * nph < r_hi; r += kColsUnroll * nph) {
         T v[kColsUnroll][VEC];
 #pragma unroll
         for (int u = 0; u < kColsUnroll; ++u) vload_nt<T, VEC>(base + (r + u * nph) * d.I, v[u]);
+        if constexpr (MODE == M_MOM) {
+          // one Welford batch of kColsUnroll rows per column
+          double f, nf;
+          uniform_weights(wkb, (double)kColsUnroll, f, nf);
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) {
+            double x[kColsUnroll];
+#pragma unroll
+            for (int u = 0; u < kColsUnroll; ++u) x[u] = to_f64(v[u][k]);
+            double mb, qb;
+            batch_moments<kColsUnroll>(x, P[k], mb, qb);
+            merge_batch(wm[k], wq[k], mb, qb, f, nf);
+          }
+          ++wkb;
+          wn += (double)kColsUnroll;
+          continue;
+        }
 #pragma unroll
         for (int u = 0; u < kColsUnroll; ++u) {
 #pragma unroll
           for (int k = 0; k < VEC; ++k) {
-            if (MODE == M_FSUM) fs[k] += to_f64(v[u][k]);
+            if (facc_mode<MODE>()) fs[k] = fop<MODE>(fs[k], to_f64(v[u][k]));
             else acc[k].add(to_f64(v[u][k]));
           }
         }
@@ -304,75 +460,110 @@ __global__ void __launch_bounds__(kThreads)
       vload_nt<T, VEC>(base + (r + nph) * d.I, v1);
       vload_nt<T, VEC>(base + (r + 2 * nph) * d.I, v2);
       vload_nt<T, VEC>(base + (r + 3 * nph) * d.I, v3);
+      double f = 0.0, nf = 0.0;
+      if (MODE == M_MOM) batch_weights(wn, 4.0, f, nf);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (MODE == M_MEAN || MODE == M_MOM) {
+        if (MODE == M_MOM) {
+          const double x[4] = {to_f64(v0[k]), to_f64(v1[k]), to_f64(v2[k]), to_f64(v3[k])};
+          double mb, qb;
+          batch_moments<4>(x, P[k], mb, qb);
+          merge_batch(wm[k], wq[k], mb, qb, f, nf);
+        } else if (MODE == M_MEAN) {
           acc[k].add(to_f64(v0[k])); acc[k].add(to_f64(v1[k]));
           acc[k].add(to_f64(v2[k])); acc[k].add(to_f64(v3[k]));
-        } else if (MODE == M_FSUM) {
-          fs[k] += to_f64(v0[k]); fs[k] += to_f64(v1[k]);
-          fs[k] += to_f64(v2[k]); fs[k] += to_f64(v3[k]);
+        } else if (facc_mode<MODE>()) {
+          fs[k] = fop<MODE>(fs[k], to_f64(v0[k])); fs[k] = fop<MODE>(fs[k], to_f64(v1[k]));
+          fs[k] = fop<MODE>(fs[k], to_f64(v2[k])); fs[k] = fop<MODE>(fs[k], to_f64(v3[k]));
         } else {
           us[k] = bop<T, MODE>(us[k], bop<T, MODE>(bop<T, MODE>(belem<T, MODE>(v0[k]), belem<T, MODE>(v1[k])),
                                                    bop<T, MODE>(belem<T, MODE>(v2[k]), belem<T, MODE>(v3[k]))));
         }
       }
+      if (MODE == M_MOM) wn += 4.0;
     }
     for (; r < r_hi; r += nph) {
       T v[VEC];
       vload_nt<T, VEC>(base + r * d.I, v);
+      if (MODE == M_MOM) wn += 1.0;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (MODE == M_MEAN || MODE == M_MOM) acc[k].add(to_f64(v[k]));
-        else if (MODE == M_FSUM) fs[k] += to_f64(v[k]);
+        if (MODE == M_MOM) {  // Welford's single-value update
+          const double x = to_f64(v[k]) - P[k];
+          const double delta = x - wm[k];
+          wm[k] += delta / wn;
+          wq[k] = fma(delta, x - wm[k], wq[k]);
+        } else if (MODE == M_MEAN) acc[k].add(to_f64(v[k]));
+        else if (facc_mode<MODE>()) fs[k] = fop<MODE>(fs[k], to_f64(v[k]));
         else us[k] = bop<T, MODE>(us[k], belem<T, MODE>(v[k]));
       }
     }
   }
 
-  // combine the row phases of each column through LDS (phase order)
-  double n_own = 0.0;
-  {
-    const int64_t span = r_hi - r_lo - ph;
-    n_own = span > 0 ? (double)((span + nph - 1) / nph) : 0.0;
+  if constexpr (MODE == M_MOM) {
+    // row phases: Chan merges in a fixed binary tree over the phases (phase
+    // p absorbs p + s at stride s), through LDS
+    for (int s = 1; s < nph; s <<= 1) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        sm0[threadIdx.x * VEC + k] = wm[k];
+        sm1[threadIdx.x * VEC + k] = wq[k];
+      }
+      smn[threadIdx.x] = wn;
+      __syncthreads();
+      if ((ph & (2 * s - 1)) == 0 && ph + s < nph) {
+        const int other = (ph + s) * d.tcv + cv;
+        const double nb = smn[other];
+        if (nb > 0.0) {
+          double f, nf;
+          batch_weights(wn, nb, f, nf);
+#pragma unroll
+          for (int k = 0; k < VEC; ++k)
+            merge_batch(wm[k], wq[k], sm0[other * VEC + k], sm1[other * VEC + k], f, nf);
+          wn += nb;
+        }
+      }
+    }
+    if (ph != 0 || !active) return;
+    const double ntot = (double)(r_hi - r_lo);
+    const int64_t plane = d.O * d.I;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const int64_t e = (int64_t)o * d.I + col0 + k;
+      const int64_t idx = sk.final_out ? e : (c * plane + e);
+      emit_mom(sk, idx, e, c, ntot, wm[k], wq[k], P[k]);
+    }
+    return;
   }
-  // mean / moment modes carry the shared-pivot sums (S1, S2) until the end
-  double m_[VEC], q_[VEC];
+
+  // other modes: combine the row phases of each column through LDS (phase
+  // order); mean carries the shared-pivot sum S1 until the end
+  double m_[VEC];
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
-    if (MODE == M_MEAN || MODE == M_MOM) { m_[k] = acc[k].s1(); q_[k] = acc[k].s2(); }
-    else if (MODE == M_FSUM) { m_[k] = fs[k]; q_[k] = 0.0; }
-    else { m_[k] = __builtin_bit_cast(double, us[k]); q_[k] = 0.0; }
+    if (MODE == M_MEAN) m_[k] = acc[k].s1();
+    else if (facc_mode<MODE>()) m_[k] = fs[k];
+    else m_[k] = __builtin_bit_cast(double, us[k]);
   }
   if (nph > 1) {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      sm0[threadIdx.x * VEC + k] = m_[k];
-      if (MODE == M_MOM) sm1[threadIdx.x * VEC + k] = q_[k];
-    }
+    for (int k = 0; k < VEC; ++k) sm0[threadIdx.x * VEC + k] = m_[k];
     __syncthreads();
     if (ph == 0) {
-      double n0 = n_own;
       for (int p = 1; p < nph; ++p) {
         const int other = p * d.tcv + cv;
-        const int64_t span = r_hi - r_lo - p;
-        const double nb = span > 0 ? (double)((span + nph - 1) / nph) : 0.0;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
           const double mb = sm0[other * VEC + k];
-          if (MODE == M_MEAN || MODE == M_MOM) {
-            m_[k] += mb;
-            if (MODE == M_MOM) q_[k] += sm1[other * VEC + k];
-          } else if (MODE == M_FSUM) {
-            m_[k] += mb;
+          if (MODE == M_MEAN || facc_mode<MODE>()) {
+            m_[k] = fop<MODE>(m_[k], mb);
           } else {
             m_[k] = __builtin_bit_cast(double, bop<T, MODE>(__builtin_bit_cast(uint64_t, m_[k]),
                                                             __builtin_bit_cast(uint64_t, mb)));
           }
         }
-        n0 += nb;
       }
-      n_own = n0;
     }
   }
   if (ph != 0 || !active) return;
@@ -380,10 +571,10 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t plane = d.O * d.I;
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
-    if (MODE == M_MEAN || MODE == M_MOM) from_sums(ntot, acc[k].K, m_[k], q_[k], m_[k], q_[k]);
+    if (MODE == M_MEAN) m_[k] = mean_from_sums(ntot, acc[k].K, m_[k]);
     const int64_t e = (int64_t)o * d.I + col0 + k;
     const int64_t idx = sk.final_out ? e : (c * plane + e);
-    emit<MODE>(sk, idx, ntot, m_[k], q_[k], __builtin_bit_cast(uint64_t, m_[k]));
+    emit<MODE>(sk, idx, ntot, m_[k], 0.0, __builtin_bit_cast(uint64_t, m_[k]));
   }
 }
 
@@ -408,31 +599,47 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t r_hi = min(d.R, r_lo + d.rchunk);
   const T *row = src + (int64_t)o * d.R;
 
-  Acc<(MODE == M_MOM) ? M_MOM : M_MEAN> acc;
+  Acc<M_MEAN> acc;
   acc.init();
-  double fs = 0.0;
+  Wel w;  // var / std
+  w.init();
+  double fs = fident<MODE>();
   uint64_t us = bident<T, MODE>();
   int64_t j = r_lo + (int64_t)lane * VEC;
   const int64_t stride = 64 * VEC;
-  // one pivot for the whole (row, chunk) -- its first element -- so the
-  // 64 lanes combine by plain sums (no per-step division, see butterfly)
-  if (MODE == M_MEAN || MODE == M_MOM) acc.pivot(to_f64(row[r_lo]));
+  // mean: one pivot for the whole (row, chunk) -- its first element -- so the
+  // 64 lanes combine by plain sums (no per-step division, see butterfly).
+  // var / std: every value is shifted by the row's first element P (shared
+  // by all chunks of the row), so the Welford means stay near zero and keep
+  // their digits on offset data (1e6 + N(0,1)); batches bound outliers.
+  if (MODE == M_MEAN) acc.pivot(to_f64(row[r_lo]));
+  const double P = (MODE == M_MOM) ? to_f64(row[0]) : 0.0;
   // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
   for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
     T v[kRowsUnroll][VEC];
 #pragma unroll
     for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
+    if constexpr (MODE == M_MOM) {
+      // the kRowsUnroll * VEC values in hand form one Welford batch
+      double x[kRowsUnroll * VEC];
+#pragma unroll
+      for (int u = 0; u < kRowsUnroll; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[u * VEC + k] = to_f64(v[u][k]);
+      w.add_main<kRowsUnroll * VEC>(x, P);
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < kRowsUnroll; ++u) {
-      if constexpr ((MODE == M_MEAN || MODE == M_MOM) && VEC % 2 == 0) {
+      if constexpr (MODE == M_MEAN && VEC % 2 == 0) {
 #pragma unroll
         for (int k = 0; k < VEC; k += 2) acc.add2(to_f64(v[u][k]), to_f64(v[u][k + 1]));
         continue;
       }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[u][k]));
-        else if (MODE == M_FSUM) fs += to_f64(v[u][k]);
+        if (MODE == M_MEAN) acc.add(to_f64(v[u][k]));
+        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(v[u][k]));
         else us = bop<T, MODE>(us, belem<T, MODE>(v[u][k]));
       }
     }
@@ -441,37 +648,47 @@ __global__ void __launch_bounds__(kThreads)
     if (j + VEC <= r_hi) {
       T v[VEC];
       vload_nt<T, VEC>(row + j, v);
+      if constexpr (MODE == M_MOM) {
+        double x[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = to_f64(v[k]);
+        w.add_batch<VEC>(x, P);
+        continue;
+      }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(v[k]));
-        else if (MODE == M_FSUM) fs += to_f64(v[k]);
+        if (MODE == M_MEAN) acc.add(to_f64(v[k]));
+        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(v[k]));
         else us = bop<T, MODE>(us, belem<T, MODE>(v[k]));
       }
     } else {
       for (int64_t k = j; k < r_hi; ++k) {
-        if (MODE == M_MEAN || MODE == M_MOM) acc.add(to_f64(row[k]));
-        else if (MODE == M_FSUM) fs += to_f64(row[k]);
+        if (MODE == M_MOM) w.add1(to_f64(row[k]) - P);
+        else if (MODE == M_MEAN) acc.add(to_f64(row[k]));
+        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(row[k]));
         else us = bop<T, MODE>(us, belem<T, MODE>(row[k]));
       }
     }
   }
 
-  // wave combination (butterfly, fixed order -> deterministic): shared
-  // pivot, so the lanes' (S1, S2) simply add; the element count is known
-  double m = acc.s1(), q = acc.s2();
-  if (MODE == M_FSUM) m = fs;
+  // wave combination (butterfly, fixed order -> deterministic).  Both lanes
+  // of a pair combine (lower lane, upper lane) in that order, so they hold
+  // identical bits afterwards.  mean: shared pivot, the S1 sums simply add;
+  // var / std: Chan merges of the lanes' Welford states.
+  double m = facc_mode<MODE>() ? fs : acc.s1();
+  double n = w.n, wm = w.mean, wq = w.m2;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    if (MODE == M_MEAN || MODE == M_MOM) {
+    if (MODE == M_MOM) {
+      const double nb = __shfl_xor(n, off), mb = __shfl_xor(wm, off), qb = __shfl_xor(wq, off);
+      const bool up = (lane & off) != 0;
+      double na = up ? nb : n, ma = up ? mb : wm, qa = up ? qb : wq;
+      chan(na, ma, qa, up ? n : nb, up ? wm : mb, up ? wq : qb, true);
+      n = na; wm = ma; wq = qa;
+    } else if (MODE == M_MEAN || facc_mode<MODE>()) {
       const double mb = __shfl_xor(m, off);
-      const double qb = (MODE == M_MOM) ? __shfl_xor(q, off) : 0.0;
-      // lower lane adds (self + partner), upper lane (partner + self):
-      // the same ordered sum on both sides of every butterfly step
-      m = (lane & off) ? (mb + m) : (m + mb);
-      if (MODE == M_MOM) q = (lane & off) ? (qb + q) : (q + qb);
-    } else if (MODE == M_FSUM) {
-      const double mb = __shfl_xor(m, off);
-      m = (lane & off) ? (mb + m) : (m + mb);
+      // lower lane combines (self, partner), upper lane (partner, self)
+      m = (lane & off) ? fop<MODE>(mb, m) : fop<MODE>(m, mb);
     } else {
       const uint64_t ub = (uint64_t)__shfl_xor((long long)us, off);
       us = (lane & off) ? bop<T, MODE>(ub, us) : bop<T, MODE>(us, ub);
@@ -479,21 +696,26 @@ __global__ void __launch_bounds__(kThreads)
   }
   if (lane != 0) return;
   const double ntot = (double)(r_hi - r_lo);
-  if (MODE == M_MEAN || MODE == M_MOM) from_sums(ntot, acc.K, m, q, m, q);
   const int64_t e = (int64_t)o;
   const int64_t idx = sk.final_out ? e : (c * d.O + e);
-  emit<MODE>(sk, idx, ntot, m, q, us);
+  if constexpr (MODE == M_MOM) {
+    emit_mom(sk, idx, e, c, ntot, wm, wq, P);
+    return;
+  }
+  if (MODE == M_MEAN) m = mean_from_sums(ntot, acc.K, m);
+  emit<MODE>(sk, idx, ntot, m, 0.0, us);
 }
 
 // --------------------------------------------------------------- combine --
+constexpr int kMaxParts = 256;  // parts per bm_reduce_combine (ranks of a merge); kernarg-resident counts
 struct CombDesc {
   int64_t nout;
   int64_t nparts;
   int64_t part_stride;  // elements between parts in a plane
   int64_t R, rchunk;    // uniform chunk counts when explicit == 0
   int32_t explicit_counts;
-  int32_t pad_;
-  int64_t counts[64];
+  int32_t pivots;       // var / std chunk partials: p0 is mean - P, P in the plane after M2
+  int64_t counts[kMaxParts];
 };
 
 template <int MODE, typename T>
@@ -511,9 +733,10 @@ __global__ void __launch_bounds__(kThreads)
       if (nb <= 0.0) continue;
       const int64_t at = p * d.part_stride + e;
       if (MODE == M_MEAN || MODE == M_MOM) {
+        // chunk partials of var / std are all around the same pivot P
         chan(n, m, q, nb, p0[at], (MODE == M_MOM) ? p1[at] : 0.0, MODE == M_MOM);
-      } else if (MODE == M_FSUM) {
-        m += p0[at];
+      } else if (facc_mode<MODE>()) {
+        m = first ? p0[at] : fop<MODE>(m, p0[at]);
         n += nb;
       } else {
         const uint64_t b = ((const uint64_t *)p0)[at];
@@ -521,7 +744,12 @@ __global__ void __launch_bounds__(kThreads)
       }
       first = false;
     }
-    emit<MODE>(sk, e, n, m, q, u);
+    if constexpr (MODE == M_MOM) {
+      const double P = d.pivots ? p1[d.nparts * d.part_stride + e] : 0.0;
+      emit_mom(sk, e, e, 1, n, m, q, P);
+    } else {
+      emit<MODE>(sk, e, n, m, q, u);
+    }
   }
 }
 
@@ -542,12 +770,32 @@ int mode_of(int stat, int dt) {
   if (stat == BM_STAT_VAR || stat == BM_STAT_STD) return M_MOM;
   if (stat == BM_STAT_MAX) return M_MAX;
   if (stat == BM_STAT_MIN) return M_MIN;
+  if (stat == BM_STAT_PROD) return is_float(dt) ? M_FPROD : (dt == BM_BOOL ? M_LAND : M_IPROD);
+  if (stat == BM_STAT_LAND) return M_LAND;
+  if (stat == BM_STAT_LOR) return M_OR;
+  if (stat == BM_STAT_BAND) return M_BAND;
+  if (stat == BM_STAT_BOR) return M_BOR;
+  if (stat == BM_STAT_BXOR) return M_BXOR;
+  if (stat == BM_STAT_FMAX) return is_float(dt) ? M_FMAX : M_MAX;
+  if (stat == BM_STAT_FMIN) return is_float(dt) ? M_FMIN : M_MIN;
   if (is_float(dt)) return M_FSUM;
   if (dt == BM_BOOL) return M_OR;
   return M_ISUM;
 }
 int planes_of(int mode) { return mode == M_MOM ? 2 : 1; }
-bool bit_mode_host(int mode) { return mode == M_ISUM || mode == M_OR || mode == M_MAX || mode == M_MIN; }
+bool bit_mode_host(int mode) {
+  return mode == M_ISUM || mode == M_OR || mode == M_MAX || mode == M_MIN || mode == M_IPROD ||
+         mode == M_LAND || mode == M_BAND || mode == M_BOR || mode == M_BXOR || mode == M_FMAX ||
+         mode == M_FMIN;
+}
+// the dtype a reduction writes: logical and / or give bool (numpy's
+// logical_* ufuncs; bool sum is OR, bool product AND), the other bit modes
+// and float sums / products keep the input dtype, statistics are float
+int out_dtype_ok(int stat, int mode, int in_dt, int out_dt) {
+  if (stat == BM_STAT_LAND || stat == BM_STAT_LOR) return out_dt == BM_BOOL;
+  if (bit_mode_host(mode)) return out_dt == in_dt;
+  return is_float(out_dt);
+}
 
 struct RedPlan {
   bool rows;
@@ -664,13 +912,13 @@ int launch_main_m(int dt, const RedPlan &p, const void *src, int64_t O, int64_t 
     case BM_U64: return launch_main_t<uint64_t, MODE>(p, src, O, R, I, sk, st);
     case BM_I64: return launch_main_t<int64_t, MODE>(p, src, O, R, I, sk, st);
     case BM_F16:
-      if constexpr (MODE != M_ISUM && MODE != M_OR) return launch_main_t<_Float16, MODE>(p, src, O, R, I, sk, st);
+      if constexpr (!int_only_mode<MODE>()) return launch_main_t<_Float16, MODE>(p, src, O, R, I, sk, st);
       break;
     case BM_F32:
-      if constexpr (MODE != M_ISUM && MODE != M_OR) return launch_main_t<float, MODE>(p, src, O, R, I, sk, st);
+      if constexpr (!int_only_mode<MODE>()) return launch_main_t<float, MODE>(p, src, O, R, I, sk, st);
       break;
     case BM_F64:
-      if constexpr (MODE != M_ISUM && MODE != M_OR) return launch_main_t<double, MODE>(p, src, O, R, I, sk, st);
+      if constexpr (!int_only_mode<MODE>()) return launch_main_t<double, MODE>(p, src, O, R, I, sk, st);
       break;
     default: break;
   }
@@ -687,6 +935,14 @@ int launch_main(int mode, int dt, const RedPlan &p, const void *src, int64_t O, 
     case M_ISUM: return launch_main_m<M_ISUM>(dt, p, src, O, R, I, sk, st);
     case M_MAX: return launch_main_m<M_MAX>(dt, p, src, O, R, I, sk, st);
     case M_MIN: return launch_main_m<M_MIN>(dt, p, src, O, R, I, sk, st);
+    case M_FPROD: return launch_main_m<M_FPROD>(dt, p, src, O, R, I, sk, st);
+    case M_IPROD: return launch_main_m<M_IPROD>(dt, p, src, O, R, I, sk, st);
+    case M_LAND: return launch_main_m<M_LAND>(dt, p, src, O, R, I, sk, st);
+    case M_BAND: return launch_main_m<M_BAND>(dt, p, src, O, R, I, sk, st);
+    case M_BOR: return launch_main_m<M_BOR>(dt, p, src, O, R, I, sk, st);
+    case M_BXOR: return launch_main_m<M_BXOR>(dt, p, src, O, R, I, sk, st);
+    case M_FMAX: return launch_main_m<M_FMAX>(dt, p, src, O, R, I, sk, st);
+    case M_FMIN: return launch_main_m<M_FMIN>(dt, p, src, O, R, I, sk, st);
     default: return launch_main_m<M_OR>(dt, p, src, O, R, I, sk, st);
   }
 }
@@ -718,16 +974,24 @@ int launch_combine(int mode, int dt, const double *p0, const double *p1, const C
     case M_MEAN: k_red_combine<M_MEAN, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
     case M_MOM: k_red_combine<M_MOM, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
     case M_FSUM: k_red_combine<M_FSUM, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_FPROD: k_red_combine<M_FPROD, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
     case M_ISUM: k_red_combine<M_ISUM, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_IPROD: k_red_combine<M_IPROD, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
     case M_OR: k_red_combine<M_OR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_LAND: k_red_combine<M_LAND, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_BAND: k_red_combine<M_BAND, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_BOR: k_red_combine<M_BOR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_BXOR: k_red_combine<M_BXOR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
     case M_MAX: launch_combine_m<M_MAX>(dt, (int)g, p0, p1, cd, sk, st); break;
+    case M_FMAX: launch_combine_m<M_FMAX>(dt, (int)g, p0, p1, cd, sk, st); break;
+    case M_FMIN: launch_combine_m<M_FMIN>(dt, (int)g, p0, p1, cd, sk, st); break;
     default: launch_combine_m<M_MIN>(dt, (int)g, p0, p1, cd, sk, st); break;
   }
   return BM_OK;
 }
 
 int check_args(int stat, int dt, int64_t O, int64_t R, int64_t I, const char *who) {
-  if (stat < BM_STAT_MEAN || stat > BM_STAT_MIN || dtype_size(dt) == 0) {
+  if (stat < BM_STAT_MEAN || stat > BM_STAT_FMIN || dtype_size(dt) == 0) {
     bm_set_error("%s: bad stat %d / dtype %d", who, stat, dt);
     return BM_E_ARG;
   }
@@ -750,7 +1014,8 @@ int check_launch(const char *who) {
 
 size_t ws_bytes_for(int mode, const RedPlan &p, int64_t nout) {
   if (p.nchunks <= 1) return 0;
-  return (size_t)planes_of(mode) * (size_t)p.nchunks * (size_t)nout * 8;
+  // var / std: + one plane of pivots
+  return ((size_t)planes_of(mode) * (size_t)p.nchunks + (mode == M_MOM ? 1 : 0)) * (size_t)nout * 8;
 }
 
 // Shared body of bm_reduce / bm_reduce_state.
@@ -775,6 +1040,8 @@ int run_reduce(int stat, const void *src, int dt, int64_t O, int64_t R, int64_t 
   part.final_out = 0;
   part.p0 = w0;
   part.p1 = w1;
+  part.p2 = w1 + (size_t)p.nchunks * nout;  // var / std pivots (ws_bytes_for reserves the plane)
+  part.shifted = mode == M_MOM;
   int rc = launch_main(mode, dt, p, src, O, R, I, part, st);
   if (rc) return rc;
   CombDesc cd{};
@@ -784,6 +1051,7 @@ int run_reduce(int stat, const void *src, int dt, int64_t O, int64_t R, int64_t 
   cd.R = R;
   cd.rchunk = p.rchunk;
   cd.explicit_counts = 0;
+  cd.pivots = mode == M_MOM;
   rc = launch_combine(mode, dt, w0, w1, cd, sk, st);
   if (rc) return rc;
   return check_launch(who);
@@ -812,10 +1080,14 @@ extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int
   if (rc) return rc;
   if (!src || !out) { bm_set_error("bm_reduce: null pointer"); return BM_E_ARG; }
   const int mode = mode_of(stat, in_dtype);
-  if (bit_mode_host(mode)) {
-    if (out_dtype != in_dtype) { bm_set_error("bm_reduce: integer sum / max / min keep the input dtype"); return BM_E_ARG; }
-  } else if (!is_float(out_dtype)) {
-    bm_set_error("bm_reduce: out_dtype must be a float dtype");
+  if (!out_dtype_ok(stat, mode, in_dtype, out_dtype)) {
+    bm_set_error("bm_reduce: out_dtype %d does not fit stat %d on dtype %d (float for statistics and "
+                 "float sums / products, bool for logical and / or, else the input dtype)",
+                 out_dtype, stat, in_dtype);
+    return BM_E_ARG;
+  }
+  if (is_float(in_dtype) && (mode == M_BAND || mode == M_BOR || mode == M_BXOR)) {
+    bm_set_error("bm_reduce: bitwise reductions need an integer or bool dtype");
     return BM_E_ARG;
   }
   Sink sk{};
@@ -828,7 +1100,7 @@ extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int
 }
 
 extern "C" int bm_reduce_state_bytes(int stat, int in_dtype, int64_t nout, size_t *bytes) {
-  if (!bytes || nout < 0 || stat < BM_STAT_MEAN || stat > BM_STAT_MIN || dtype_size(in_dtype) == 0) {
+  if (!bytes || nout < 0 || stat < BM_STAT_MEAN || stat > BM_STAT_FMIN || dtype_size(in_dtype) == 0) {
     bm_set_error("bm_reduce_state_bytes: bad arguments");
     return BM_E_ARG;
   }
@@ -856,16 +1128,20 @@ extern "C" int bm_reduce_state(int stat, const void *src, int in_dtype, int64_t 
 
 extern "C" int bm_reduce_combine(int stat, int in_dtype, const void *states, const int64_t *counts,
                                  int nparts, int64_t nout, void *out, int out_dtype, void *stream) {
-  if (stat < BM_STAT_MEAN || stat > BM_STAT_MIN || dtype_size(in_dtype) == 0 || nparts < 1 ||
-      nparts > 64 || nout < 1 || !states || !counts || !out) {
+  if (stat < BM_STAT_MEAN || stat > BM_STAT_FMIN || dtype_size(in_dtype) == 0 || nparts < 1 ||
+      nparts > kMaxParts || nout < 1 || !states || !counts || !out) {
     bm_set_error("bm_reduce_combine: bad arguments");
     return BM_E_ARG;
   }
   const int mode = mode_of(stat, in_dtype);
-  if (bit_mode_host(mode)) {
-    if (out_dtype != in_dtype) { bm_set_error("bm_reduce_combine: integer sum / max / min keep the input dtype"); return BM_E_ARG; }
-  } else if (!is_float(out_dtype)) {
-    bm_set_error("bm_reduce_combine: out_dtype must be a float dtype");
+  if (!out_dtype_ok(stat, mode, in_dtype, out_dtype)) {
+    bm_set_error("bm_reduce_combine: out_dtype %d does not fit stat %d on dtype %d (float for statistics and "
+                 "float sums / products, bool for logical and / or, else the input dtype)",
+                 out_dtype, stat, in_dtype);
+    return BM_E_ARG;
+  }
+  if (is_float(in_dtype) && (mode == M_BAND || mode == M_BOR || mode == M_BXOR)) {
+    bm_set_error("bm_reduce_combine: bitwise reductions need an integer or bool dtype");
     return BM_E_ARG;
   }
   CombDesc cd{};

@@ -74,3 +74,9 @@ def ones(*args, **kwargs):
 def zeros(*args, **kwargs):
     """Create a bolt array of zeros."""
     return lookup(*args, **kwargs).dispatch('zeros', *args, **_strip_mode(kwargs))
+
+
+@wrapped
+def concatenate(*args, **kwargs):
+    """Join two bolt arrays (factory.py:78-83)."""
+    return lookup(*args, **kwargs).dispatch('concatenate', *args, **_strip_mode(kwargs))

@@ -57,3 +57,11 @@ class ConstructLocal(ConstructBase):
     @staticmethod
     def zeros(shape, dtype=np.float64, order='C'):
         return BoltArrayLocal(np.zeros(shape, dtype, order))
+
+    @staticmethod
+    def concatenate(arrays, axis=0):
+        """numpy.concatenate of a tuple of arrays (bolt/local/construct.py:85-105)."""
+        if not isinstance(arrays, tuple):
+            raise ValueError("data type not understood")
+        arrays = tuple([np.asarray(a) for a in arrays])
+        return BoltArrayLocal(np.concatenate(arrays, axis))

@@ -12,6 +12,9 @@ ABI_VERSION = 1
 
 BM_BOOL, BM_U8, BM_I8, BM_U16, BM_I16, BM_U32, BM_I32, BM_U64, BM_I64, BM_F16, BM_F32, BM_F64 = range(12)
 STAT_MEAN, STAT_VAR, STAT_STD, STAT_SUM, STAT_MAX, STAT_MIN = range(6)
+# reduce(func) with numpy ufuncs (include/bolt_mi355x.h BM_STAT_PROD..BM_STAT_FMIN)
+STAT_PROD, STAT_LAND, STAT_LOR, STAT_BAND, STAT_BOR, STAT_BXOR, STAT_FMAX, STAT_FMIN = range(6, 14)
+MAX_COMBINE_PARTS = 256  # bm_reduce_combine's nparts limit (ranks of one merge)
 
 LIB_PATH = os.environ.get("BOLT_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libbolt_mi355x.so")  # env: A/B builds
@@ -41,7 +44,17 @@ SIGNATURES = {
                                    _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     "bm_reduce_combine": (_c.c_int, [_c.c_int, _c.c_int, _c.c_void_p, _i64p, _c.c_int, _c.c_int64,
                                      _c.c_void_p, _c.c_int, _c.c_void_p]),
+    "bm_comm_unique_id": (_c.c_int, [_c.c_void_p, _c.c_size_t]),
+    "bm_comm_init": (_c.c_int, [_c.POINTER(_c.c_void_p), _c.c_int, _c.c_void_p, _c.c_int]),
+    "bm_comm_destroy": (_c.c_int, [_c.c_void_p]),
+    "bm_comm_info": (_c.c_int, [_c.c_void_p, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int), _c.c_char_p,
+                                _c.c_size_t]),
+    "bm_alltoallv": (_c.c_int, [_c.c_void_p, _c.c_void_p, _i64p, _i64p, _c.c_void_p, _i64p, _i64p,
+                                _c.c_void_p]),
+    "bm_allgatherv": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_void_p, _i64p, _i64p,
+                                 _c.c_void_p]),
 }
+COMM_ID_BYTES = 128  # BM_COMM_ID_BYTES
 
 _LIB = None
 

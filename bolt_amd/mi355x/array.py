@@ -28,9 +28,49 @@ from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, permute_
 from bolt_amd.mi355x.transfer import finish_host_result, host_result, to_device, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
-from bolt_amd.utils import tupleize, argpack, inshape, istransposeable
+from bolt_amd.utils import tupleize, argpack, inshape, istransposeable, isreshapeable
 
 _STAT_CODES = {'mean': _lib.STAT_MEAN, 'variance': _lib.STAT_VAR, 'stdev': _lib.STAT_STD}
+
+
+def _ufunc_stats():
+    """reduce(func) functions that run as one bm_reduce mode (array.py:243-282)."""
+    import operator
+    return {operator.add: _lib.STAT_SUM, np.add: _lib.STAT_SUM,
+            np.maximum: _lib.STAT_MAX, np.minimum: _lib.STAT_MIN,
+            operator.mul: _lib.STAT_PROD, np.multiply: _lib.STAT_PROD,
+            np.logical_and: _lib.STAT_LAND, np.logical_or: _lib.STAT_LOR,
+            np.bitwise_and: _lib.STAT_BAND, operator.and_: _lib.STAT_BAND,
+            np.bitwise_or: _lib.STAT_BOR, operator.or_: _lib.STAT_BOR,
+            np.bitwise_xor: _lib.STAT_BXOR, operator.xor: _lib.STAT_BXOR,
+            np.fmax: _lib.STAT_FMAX, np.fmin: _lib.STAT_FMIN}
+
+
+_UFUNC_STATS = _ufunc_stats()
+
+
+def _hashable(f):
+    try:
+        hash(f)
+        return True
+    except TypeError:
+        return False
+
+
+def _tree(func, recs):
+    """((r0 f r1) f (r2 f r3)) ... over the leading axis of a device tensor."""
+    import torch
+    from bolt_amd.mi355x.functional import apply_pairs
+    while recs.shape[0] > 1:
+        n = recs.shape[0]
+        nxt = apply_pairs(func, recs[0:n - 1:2], recs[1:n:2])
+        if n % 2:
+            nxt = torch.cat([nxt, recs[n - 1:].to(nxt.dtype)])
+        recs = nxt
+    return recs[0]
+# reductions whose result keeps the input dtype (numpy's same-dtype ufunc rule)
+_KEEP_DTYPE = (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN, _lib.STAT_PROD, _lib.STAT_BAND,
+               _lib.STAT_BOR, _lib.STAT_BXOR, _lib.STAT_FMAX, _lib.STAT_FMIN)
 
 
 @functools.lru_cache(maxsize=256)
@@ -103,14 +143,34 @@ class BoltArrayMI355X(BoltArray):
         rowbytes = int(np.prod(shape[1:], dtype=np.int64)) * es
         if identity:
             data = to_device(arry[lo:hi].reshape(-1).view(np.uint8), dev)
-        else:
-            # full array to HBM, permuted on the GPU, then this rank's slab of
-            # the permuted bytes (the reference's reshape to the old shape).
+        elif ctx.world_size == 1:
+            # whole array to HBM, permuted on the GPU (the reference's records
+            # are x.transpose(perm) reshaped to the old shape)
             full = to_device(arry.reshape(-1).view(np.uint8), dev)
-            perm_bytes = _empty(full.numel(), dev)
+            data = _empty(full.numel(), dev)
             if full.numel():
-                backend_for(dev).permute(full, arry.shape, permutation, es, perm_bytes)
-            data = perm_bytes[lo * rowbytes:hi * rowbytes].clone() if ctx.world_size > 1 else perm_bytes
+                backend_for(dev).permute(full, arry.shape, permutation, es, data)
+        else:
+            # this rank's slab is the flat element range [s, e) of
+            # x.transpose(perm): upload only the source planes along axis
+            # perm[0] that cover it, permute them on the GPU, cut the range
+            pshape = tuple(arry.shape[i] for i in permutation)
+            inner0 = int(np.prod(pshape[1:], dtype=np.int64))
+            s0, e0 = lo * (rowbytes // es), hi * (rowbytes // es)
+            if e0 == s0 or inner0 == 0:
+                data = _empty(0, dev)
+            else:
+                i_lo, i_hi = s0 // inner0, min(pshape[0], -(-e0 // inner0))
+                idx = [slice(None)] * arry.ndim
+                idx[permutation[0]] = slice(i_lo, i_hi)
+                sub = np.ascontiguousarray(arry[tuple(idx)])
+                part = to_device(sub.reshape(-1).view(np.uint8), dev)
+                perm_bytes = _empty(part.numel(), dev)
+                backend_for(dev).permute(part, sub.shape, permutation, es, perm_bytes)
+                off = (s0 - i_lo * inner0) * es
+                data = perm_bytes[off:off + (e0 - s0) * es]
+                if data.numel() != perm_bytes.numel():
+                    data = data.clone()
         return cls(data, shape=shape, split=split, dtype=dtype, context=ctx, npartitions=npartitions)
 
     @classmethod
@@ -202,10 +262,13 @@ class BoltArrayMI355X(BoltArray):
         return Values(self)
 
     def cache(self):
-        """No-op: records are resident in HBM (array.py:37-41)."""
+        """Records are resident in HBM already (array.py:37-41); only the flag
+        the record view reports changes."""
+        self._cached = True
 
     def unpersist(self):
-        """No-op (array.py:43-47)."""
+        """(array.py:43-47) -- the records stay in HBM; clears the flag."""
+        self._cached = False
 
     # ------------------------------------------------------------ movement
     def _permute(self, perm, split):
@@ -308,6 +371,76 @@ class BoltArrayMI355X(BoltArray):
         p[axis2] = axis1
         return self.transpose(p)
 
+    def reshape(self, *shape):
+        """Same data, new shape (array.py:835-877): only reshapes that split into
+        an independent reshape of the keys and one of the values
+        (NotImplementedError otherwise, as the reference).  On the dense
+        layout both are metadata, plus a re-slab across GPUs when the leading
+        key axis changes (shapes.py:40-64, :111-134)."""
+        new = argpack(shape)
+        isreshapeable(new, self.shape)
+        if new == self.shape:
+            return self
+        i = self._reshapebasic(new)
+        if i == -1:
+            raise NotImplementedError("Currently no support for reshaping between "
+                                      "keys and values for BoltArraySpark")
+        return self.keys.reshape(new[:i]).values.reshape(new[i:])
+
+    def _reshapebasic(self, shape):
+        """Index in ``shape`` splitting it into key and value parts of the old
+        key and value sizes, or -1 (array.py:861-877)."""
+        new = tupleize(shape)
+        old_key = int(np.prod(self.keys.shape, dtype=np.int64))
+        old_val = int(np.prod(self.values.shape, dtype=np.int64))
+        for i in range(len(new)):
+            if int(np.prod(new[:i], dtype=np.int64)) == old_key and \
+                    int(np.prod(new[i:], dtype=np.int64)) == old_val:
+                return i
+        return -1
+
+    def astype(self, dtype, casting='unsafe'):
+        """Cast every record to ``dtype`` (array.py:920-930), on the device.
+
+        numpy's casting rule is checked on the host (np.can_cast raises the
+        same TypeError numpy's astype would); the conversion itself is torch's
+        elementwise cast, numpy's values for every finite in-range input."""
+        from bolt_amd.mi355x import functional as F
+        dtype = np.dtype(dtype)
+        if not np.can_cast(self._dtype, dtype, casting):
+            raise TypeError("Cannot cast array data from %r to %r according to the rule %r"
+                            % (self._dtype, dtype, casting))
+        if dtype == self._dtype:
+            return self._like(self._data.clone(), self._shape, self._split)
+        src = F.view(self._data, (self._data.numel() // max(1, self._dtype.itemsize),), self._dtype)
+        out = F.as_bytes(src.to(F.torch_dtype(dtype)))
+        return self._like(out, self._shape, self._split, dtype=dtype)
+
+    def clip(self, min=None, max=None):
+        """Clip values below ``min`` / above ``max`` (array.py:932-945), on the device."""
+        import torch
+        from bolt_amd.mi355x import functional as F
+        src = F.view(self._data, self._local_shape, self._dtype)
+        out = src.clone()
+        vs = tuple(self._shape[self._split:])
+        for bound, fn in ((min, torch.maximum), (max, torch.minimum)):
+            if bound is None:
+                continue
+            b = torch.as_tensor(np.asarray(bound, dtype=self._dtype), device=out.device)
+            if b.ndim > len(vs):
+                raise ValueError("clip bound of shape %s does not broadcast to records %s" % (b.shape, vs))
+            out = fn(out, b)
+        return self._like(F.as_bytes(out), self._shape, self._split)
+
+    def repartition(self, npartitions):
+        """Records stay sharded one slab per GPU; only the partition count the
+        array reports changes, and, as after Spark's repartition, the array is
+        marked unordered (array.py:49-60)."""
+        out = self._like(self._data, self._shape, self._split)
+        out._npartitions = npartitions
+        out._ordered = False
+        return out
+
     # ---------------------------------------------------------- functional
     def stack(self, size=None):
         """Group each partition's records into stacks of up to ``size`` (array.py:62-83)."""
@@ -354,7 +487,7 @@ class BoltArrayMI355X(BoltArray):
         axis = tupleize(axis)
         swapped = self._align(axis)
         dev = swapped._data.device
-        test_func = (lambda x: func(((0,), x))) if with_keys else func
+        test_func = (lambda x: func((F.KeyTuple((0,) * len(axis)), x))) if with_keys else func
         if value_shape is None or dtype is None:
             try:
                 mapped = F.to_device(test_func(F.random_like(swapped.values.shape, self._dtype, dev)), dev)
@@ -373,7 +506,7 @@ class BoltArrayMI355X(BoltArray):
             lo, _ = swapped._ctx.local_bounds(swapped._shape[0]) if swapped._shape else (0, 0)
             kshape = swapped._shape[:swapped._split]
             base = lo * int(np.prod(kshape[1:], dtype=np.int64))
-            outs = [F.to_device(func((tuple(int(k) for k in np.unravel_index(base + i, kshape)), recs[i])), dev)
+            outs = [F.to_device(func((F.KeyTuple(int(k) for k in np.unravel_index(base + i, kshape)), recs[i])), dev)
                     for i in range(recs.shape[0])]
             out = torch.stack(outs) if outs else None
         else:
@@ -400,11 +533,13 @@ class BoltArrayMI355X(BoltArray):
         ctx = swapped._ctx
         local_idx = np.nonzero(mask)[0].astype(np.int64)
         if ctx.world_size > 1:
-            import torch.distributed as dist
-            allm = [None] * ctx.world_size
-            dist.all_gather_object(allm, mask, group=ctx.group)
-            offs = np.r_[0, np.cumsum([m.size for m in allm])]
-            glob = np.concatenate([np.nonzero(m)[0] + offs[r] for r, m in enumerate(allm)]).astype(np.int64)
+            # every rank's mask (one byte per record, rank order) on every rank
+            import torch
+            per = int(np.prod(swapped.shape[1:swapped.split], dtype=np.int64))
+            sizes = [(hi - lo) * per for lo, hi in ctx.bounds(swapped.shape[0])]
+            mb = torch.from_numpy(mask.astype(np.uint8)).to(swapped._data.device)
+            allm = all_gather_bytes(ctx, mb, sizes).cpu().numpy()
+            glob = np.nonzero(allm)[0].astype(np.int64)
         else:
             glob = local_idx
         remaining = list(swapped.shape[len(axis):])
@@ -555,8 +690,10 @@ class BoltArrayMI355X(BoltArray):
             axset = sorted(set(int(a) for a in axis))
             kept = [i for i in range(self.ndim) if i not in axset]
             out_shape = tuple(self._shape[i] for i in kept)
-            if stat in (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN):
+            if stat in _KEEP_DTYPE:
                 out_dtype = self._dtype
+            elif stat in (_lib.STAT_LAND, _lib.STAT_LOR):
+                out_dtype = np.dtype(bool)
             else:
                 out_dtype = stat_dtype(self._dtype, out_shape)
             perm, O, R, I = reduce_layout(lshape, axset)
@@ -598,6 +735,11 @@ class BoltArrayMI355X(BoltArray):
         # the sharded axis is reduced: per-rank states, gathered and combined
         # in rank order (statcounter.py:67-99, deterministic here)
         nout = int(np.prod(out_shape, dtype=np.int64))
+        if nout == 0:  # e.g. mean(axis=0) of (4, 0, 3): nothing to merge
+            return np.empty(out_shape, out_dtype), out_dtype
+        if ctx.world_size > _lib.MAX_COMBINE_PARTS:
+            raise NotImplementedError("reductions over the sharded axis merge at most %d ranks (got %d)"
+                                      % (_lib.MAX_COMBINE_PARTS, ctx.world_size))
         sbytes = be.state_bytes(stat, code, nout)
         state = _empty(sbytes, dev)
         count = int(np.prod([lshape[i] for i in axset], dtype=np.int64))
@@ -643,20 +785,29 @@ class BoltArrayMI355X(BoltArray):
     def reduce(self, func, axis=(0,), keepdims=False):
         """Reduce with ``func`` over ``axis`` (array.py:243-282).
 
-        The reductions sum/max/min take -- operator.add / numpy.add,
-        numpy.maximum, numpy.minimum -- run on the GPU in the input dtype;
-        arbitrary Python functions are outside this backend.
+        The reference treeReduces ``func`` over the aligned records.  numpy
+        ufuncs (add, multiply, maximum, minimum, fmax, fmin, logical_and /
+        or, bitwise_and / or / xor and their ``operator`` spellings) run as
+        one bm_reduce mode on the GPU, with numpy's result dtype for
+        ``func(record, record)``; any other binary function receives device
+        tensors and is applied as a pairwise tree in record order,
+        ((r0 f r1) f (r2 f r3)) ..., vmapped over the pairs of each level.
+        A single record is returned as is, as treeReduce returns it.
         """
-        import operator
-        stat = {operator.add: _lib.STAT_SUM, np.add: _lib.STAT_SUM,
-                np.maximum: _lib.STAT_MAX, np.minimum: _lib.STAT_MIN}.get(func)
-        if stat is None:
-            raise NotImplementedError("the mi355x mode reduces with add / maximum / minimum; got %r" % (func,))
         axis = tupleize(axis)
         inshape(self.shape, axis)
-        if self._nrecords(axis) == 0:
+        nrec = self._nrecords(axis)
+        if nrec == 0:
             raise ValueError("Can not reduce() empty RDD")  # treeReduce of no records (array.py:269)
-        arr, _ = self._reduced(axis, stat)
+        stat = _UFUNC_STATS.get(func) if _hashable(func) else None
+        if nrec == 1:
+            # treeReduce of one record returns it untouched (no func call)
+            kept = [d for i, d in enumerate(self._shape) if i not in set(int(a) for a in axis)]
+            arr = self.toarray().reshape(kept)
+        elif stat is not None and self._reduce_dtype_ok(func, stat):
+            arr, _ = self._reduced(axis, stat)
+        else:
+            arr = self._tree_reduce(func, axis)
         if arr.ndim == 0:
             arr = arr[()]
         if keepdims:
@@ -667,6 +818,56 @@ class BoltArrayMI355X(BoltArray):
         elif arr.shape == (1,):
             return arr[0]
         return BoltArrayLocal(arr)
+
+    def _reduce_dtype_ok(self, func, stat):
+        """numpy's own rule for func(record, record) (raises numpy's TypeError for
+        bitwise ufuncs on floats); True if the kernel mode produces that dtype."""
+        probe = np.asarray(func(np.zeros(1, self._dtype), np.zeros(1, self._dtype)))
+        want = np.dtype(bool) if stat in (_lib.STAT_LAND, _lib.STAT_LOR) else self._dtype
+        return probe.dtype == want
+
+    def _tree_reduce(self, func, axis):
+        """Pairwise tree of a user function over the aligned records, on the device."""
+        import torch
+        from bolt_amd.mi355x.functional import view, apply_pairs, numpy_dtype
+        ctx = self._ctx
+        axset = sorted(set(int(a) for a in axis))
+        kept = [i for i in range(self.ndim) if i not in axset]
+        lshape = self._local_shape
+        perm, O, R, I = reduce_layout(lshape, axset)
+        src = self._data
+        if perm is not None:
+            tmp = _empty(src.numel(), src.device)
+            if src.numel():
+                self._backend.permute(src, lshape, perm, self._dtype.itemsize, tmp)
+            src = tmp
+        rec_shape = tuple(lshape[i] for i in kept)
+        recs = view(src, (O, R, I), self._dtype).permute(1, 0, 2).reshape((R,) + rec_shape)
+        if R:
+            part = _tree(func, recs)
+        else:
+            # a rank with no records still needs the result's dtype and shape
+            z = torch.zeros((1,) + rec_shape, dtype=recs.dtype, device=recs.device)
+            part = apply_pairs(func, z, z)[0]
+        out_dtype = numpy_dtype(part.dtype)
+        if ctx.world_size == 1:
+            return part.cpu().numpy().astype(out_dtype, copy=False)
+        from bolt_amd.mi355x.functional import as_bytes
+        if 0 not in axset:
+            # every rank reduced its own slab of outputs: gather them in rank order
+            out_shape = tuple(self._shape[i] for i in kept)
+            sizes = [int(np.prod((hi - lo,) + out_shape[1:], dtype=np.int64)) * out_dtype.itemsize
+                     for lo, hi in ctx.bounds(self._shape[0])]
+            got = all_gather_bytes(ctx, as_bytes(part.to(recs.device)), sizes)
+            return to_host(got, out_dtype, out_shape)
+        # the sharded axis is reduced: rank partials, then the same tree over
+        # the ranks that hold records, in rank order
+        pbytes = as_bytes(part)
+        allp = all_gather_bytes(ctx, pbytes, [pbytes.numel()] * ctx.world_size)
+        per = view(allp, (ctx.world_size,) + tuple(part.shape), out_dtype)
+        has = [r for r, (lo, hi) in enumerate(ctx.bounds(self._shape[0])) if hi > lo]
+        res = _tree(func, per[has])
+        return res.cpu().numpy().astype(numpy_dtype(res.dtype), copy=False)
 
     def _nrecords(self, axis):
         """Records the reduction sees after _align: the product of the reduced extents."""
@@ -730,7 +931,14 @@ class BoltArrayMI355X(BoltArray):
 
     def tordd(self):
         from bolt_amd.mi355x.records import RecordView
-        return RecordView(list(self.records()), self._ctx.world_size)
+        return RecordView(list(self.records()), self._npartitions or self._ctx.world_size,
+                          cached=getattr(self, "_cached", False))
+
+    @property
+    def _rdd(self):
+        """A host view of the records (RecordView), for code written against
+        the Spark mode's ``_rdd`` (collect, map, sortByKey, ...)."""
+        return self.tordd()
 
     def __repr__(self):
         s = "BoltArray\n"

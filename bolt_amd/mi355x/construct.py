@@ -76,6 +76,23 @@ class ConstructMI355X(ConstructBase):
                                            dtype, context, npartitions)
 
     @staticmethod
+    def concatenate(arrays, axis=0):
+        """Join two arrays, at least one of them an mi355x array (spark/construct.py:136-167)."""
+        from bolt_amd.mi355x.array import BoltArrayMI355X
+        if not isinstance(arrays, tuple):
+            raise ValueError("data type not understood")
+        if not len(arrays) == 2:
+            raise NotImplementedError("spark concatenation only supports two arrays")
+        first, second = arrays
+        if isinstance(first, BoltArrayMI355X):
+            return first.concatenate(second, axis)
+        elif isinstance(second, BoltArrayMI355X):
+            first = ConstructMI355X.array(first, second.context)
+            return first.concatenate(second, axis)
+        else:
+            raise ValueError("at least one array must be a spark bolt array")
+
+    @staticmethod
     def _argcheck(*args, **kwargs):
         """True when an argument is an MI355XContext or BoltArrayMI355X (spark/construct.py:169-190)."""
         from bolt_amd.mi355x.array import BoltArrayMI355X

@@ -2,10 +2,14 @@
 
 Plays the role SparkContext plays for the spark mode
 (bolt/spark/construct.py:24-25, :69): it names where records live.  One
-process drives one GPU; with torch.distributed initialised (backend 'nccl' =
-RCCL over xGMI on MI355X) the records of every array are sharded over the
-ranks along the leading key axis, in contiguous slabs as numpy.array_split
-would cut them (the analogue of parallelize's contiguous partitions).
+process drives one GPU; with torch.distributed initialised the records of
+every array are sharded over the ranks along the leading key axis, in
+contiguous slabs as numpy.array_split would cut them (the analogue of
+parallelize's contiguous partitions).  Over an nccl process group the
+context opens its own RCCL communicator in libbolt_mi355x (bm_comm_init; the
+id travels through the group's rendezvous store) and every record exchange
+goes through it; torch.distributed is used for rendezvous and host-side
+metadata only.
 """
 import os
 
@@ -15,6 +19,7 @@ import numpy as np
 class MI355XContext(object):
 
     _default = None
+    _ncomm = 0  # communicators created by this process (names their rendezvous keys)
 
     def __init__(self, device=None, group=None):
         import torch
@@ -38,6 +43,44 @@ class MI355XContext(object):
         # (no HIP device / library): the mode has no CPU fallback
         from bolt_amd.mi355x._ops import backend_for
         self.backend = backend_for(self.device)
+        # RCCL communicator of libbolt_mi355x (bm_comm_init) for the record
+        # exchanges when the ranks drive GPUs over an nccl (= RCCL) group
+        self.comm = None
+        self.comm_stream = None
+        if self.world_size > 1 and self.device.type == "cuda" and dist.get_backend(group) == "nccl":
+            self._init_comm()
+
+    def _init_comm(self):
+        """One RCCL communicator over this context's ranks: rank 0 makes the id,
+        the others read it from the torch.distributed rendezvous store."""
+        import ctypes
+        import torch
+        import torch.distributed as dist
+        from bolt_amd.mi355x import _lib
+        lib = _lib.load()
+        MI355XContext._ncomm += 1
+        key = "bolt_amd/rccl_id/%d" % MI355XContext._ncomm
+        uid = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+        store = dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            _lib.check(lib.bm_comm_unique_id(uid, _lib.COMM_ID_BYTES), "bm_comm_unique_id")
+            store.set(key, uid.raw)
+        else:
+            raw = store.get(key)
+            ctypes.memmove(uid, raw, _lib.COMM_ID_BYTES)
+        comm = ctypes.c_void_p()
+        _lib.check(lib.bm_comm_init(ctypes.byref(comm), self.world_size, uid, self.rank), "bm_comm_init")
+        self.comm = comm.value
+        self.comm_stream = torch.cuda.Stream(self.device)
+
+    def close(self):
+        """Release the RCCL communicator (before the process group is destroyed)."""
+        if self.comm is not None:
+            from bolt_amd.mi355x import _lib
+            import torch
+            torch.cuda.synchronize(self.device)
+            _lib.check(_lib.load().bm_comm_destroy(self.comm), "bm_comm_destroy")
+            self.comm = None
 
     @classmethod
     def default(cls):

@@ -4,11 +4,15 @@ The Spark path moves records with two shuffles and a driver collect
 (bolt/spark/chunk.py:251-261 partitionBy in keys_to_values, chunk.py:179-191
 in unchunk, array.py:1012-1014 collect).  Here records are slabs of the
 leading key axis, one slab per rank, and the only exchange a swap needs is
-ONE all-to-all (torch.distributed over RCCL, i.e. xGMI peer links):
+ONE all-to-all over RCCL (xGMI peer links), issued by libbolt_mi355x itself
+(bm_alltoallv / bm_allgatherv on the context's communicator; torch only owns
+the buffers and streams).  Over a gloo process group (the CPU tests and the
+one-GPU multi-rank rehearsal) the same exchanges use torch.distributed:
 
   pack    local strided copy of the shard into G contiguous send blocks,
           block q = the part of the permuted array that rank q will own;
-  a2a     all_to_all_single with per-peer byte counts;
+  a2a     bm_alltoallv with per-peer byte counts (one RCCL group of
+          ncclSend / ncclRecv pairs, every link at once);
   unpack  local strided copy of each received block into its place.
 
 A permutation that keeps the leading axis (perm[0] == 0) needs no exchange.
@@ -30,6 +34,7 @@ from bolt_amd.mi355x.transfer import to_host  # noqa: E402,F401  (re-exported)
 # Pipeline depth of the swap exchange (None: from the message size, >= 32 MiB
 # per peer per stage, at most 8 stages); tests set it to exercise the stages.
 STAGES = None
+STAGE_BYTES = 32 << 20  # per-peer bytes of one stage (tests lower it)
 
 # Optional phase timing of the exchange (bench.py sets it to a dict):
 # name -> list of (start, end) torch.cuda.Event pairs on the current stream.
@@ -83,12 +88,70 @@ def _host_staged(ctx, t):
     return t.device.type == "cuda" and dist.get_backend(ctx.group) == "gloo"
 
 
+class _Work(object):
+    """An exchange running on the context's RCCL stream: wait() orders the
+    caller's current stream after it (the host never blocks)."""
+
+    def __init__(self, done):
+        self.done = done
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream().wait_event(self.done)
+
+
+def _offsets(sizes):
+    return [int(v) for v in np.r_[0, np.cumsum([int(v) for v in sizes])][:-1]]
+
+
+def _rccl_all_gather(ctx, local, sizes):
+    """bm_allgatherv on the current stream (include/bolt_mi355x.h)."""
+    import torch
+    from bolt_amd.mi355x import _lib
+    recv = _empty(sum(sizes), local.device)
+    stream = torch.cuda.current_stream(local.device).cuda_stream
+    sp = local.data_ptr() if local.numel() else None
+    rp = recv.data_ptr() if recv.numel() else None
+    _lib.check(_lib.load().bm_allgatherv(ctx.comm, sp, int(sizes[ctx.rank]), rp, _lib.i64_array(sizes),
+                                         _lib.i64_array(_offsets(sizes)), stream), "bm_allgatherv")
+    return recv
+
+
+def _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op):
+    """bm_alltoallv; async: on the context's RCCL stream, fenced by events."""
+    import torch
+    from bolt_amd.mi355x import _lib
+    recv = _empty(sum(recv_sizes), send.device)
+    cur = torch.cuda.current_stream(send.device)
+    stream = ctx.comm_stream if async_op else cur
+    if async_op:
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        stream.wait_event(ready)
+        # the buffers are used on the RCCL stream: keep the allocator from
+        # reusing them before it is done
+        send.record_stream(stream)
+        recv.record_stream(stream)
+    sp = send.data_ptr() if send.numel() else None
+    rp = recv.data_ptr() if recv.numel() else None
+    _lib.check(_lib.load().bm_alltoallv(ctx.comm, sp, _lib.i64_array(send_sizes), _lib.i64_array(_offsets(send_sizes)),
+                                        rp, _lib.i64_array(recv_sizes), _lib.i64_array(_offsets(recv_sizes)),
+                                        stream.cuda_stream), "bm_alltoallv")
+    if not async_op:
+        return recv
+    done = torch.cuda.Event()
+    done.record(stream)
+    return recv, _Work(done)
+
+
 def all_gather_bytes(ctx, local, sizes):
     """Concatenate every rank's byte tensor (sizes[r] bytes from rank r) on every rank."""
     import torch
     import torch.distributed as dist
     if ctx.world_size == 1:
         return local
+    if ctx.comm is not None:
+        return _rccl_all_gather(ctx, local, sizes)
     if _host_staged(ctx, local):
         return all_gather_bytes(ctx, local.cpu(), sizes).to(local.device)
     m = max(sizes) if sizes else 0
@@ -110,6 +173,8 @@ def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1, async_op=False):
     collective's own stream and ``work.wait()`` orders the caller's stream
     after it (no host block on RCCL)."""
     import torch.distributed as dist
+    if ctx.comm is not None:
+        return _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op)
     if _host_staged(ctx, send):
         recv = all_to_all_bytes(ctx, send.cpu(), send_sizes, recv_sizes, unit).to(send.device)
         return (recv, None) if async_op else recv
@@ -161,8 +226,11 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
     # Pipeline the exchange in K stages along the output rows: stage k packs
     # its sub-blocks, starts its all-to-all asynchronously (RCCL stream) and,
     # while that runs, the current stream unpacks stage k-1 and packs k+1.
-    per_peer = (in_hi - in_lo) * int(np.prod(shape[1:])) * es // G
-    K = STAGES if STAGES else int(max(1, min(8, per_peer // (32 << 20))))
+    # K must agree on every rank (each stage is one collective), so it comes
+    # from global quantities only: the largest slab's per-peer block
+    max_rows = max(hi_ - lo_ for lo_, hi_ in in_b)
+    per_peer = max_rows * int(np.prod(shape[1:])) * es // G
+    K = STAGES if STAGES else int(max(1, min(8, per_peer // STAGE_BYTES)))
     K = max(1, min(K, min(b - a_ for a_, b in out_b) or 1))
 
     def sub(q, k):

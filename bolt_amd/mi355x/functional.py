@@ -93,3 +93,60 @@ def apply_batched(func, batch):
     if len(shapes) != 1:
         raise Exception("Map operation did not produce values of uniform shape.")
     return torch.stack(outs)
+
+
+def apply_pairs(func, a, b):
+    """stack([func(a[i], b[i]) for i]) -- a user reduce function over record
+    pairs, vmapped when the function allows it (else one pair at a time)."""
+    import torch
+    if a.shape[0] == 0:
+        try:
+            from torch.func import vmap
+            out = vmap(func)(a, b)
+            if isinstance(out, torch.Tensor):
+                return out
+        except Exception:
+            pass
+        z = torch.zeros((1,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device)
+        return to_device(func(z[0], z[0]), a.device)[None][:0]
+    try:
+        from torch.func import vmap
+        out = vmap(func)(a, b)
+        if isinstance(out, torch.Tensor) and out.shape[0] == a.shape[0]:
+            return out
+    except Exception:
+        pass
+    outs = [to_device(func(a[i], b[i]), a.device) for i in range(a.shape[0])]
+    return torch.stack(outs)
+
+
+class KeyTuple(tuple):
+    """A record key handed to a ``with_keys`` user function: a plain tuple of
+    ints (indexable, hashable) that, like a tuple meeting a numpy array in
+    the reference (array.py:125-191 passes (key, ndarray) pairs), combines
+    arithmetically with a device tensor: ``k + v`` adds the key broadcast
+    against the value instead of raising tuple's concatenation TypeError."""
+
+    def _t(self, other):
+        import torch
+        return torch.as_tensor(tuple(self), device=other.device)
+
+    def _op(name, reflected=False):
+        def f(self, other):
+            import torch
+            if isinstance(other, torch.Tensor):
+                a, b = (other, self._t(other)) if reflected else (self._t(other), other)
+                return getattr(a, name)(b)
+            return getattr(super(KeyTuple, self), "__r%s__" % name[2:-2] if reflected else name,
+                           lambda o: NotImplemented)(other)
+        return f
+
+    __add__ = _op("__add__")
+    __radd__ = _op("__add__", reflected=True)
+    __sub__ = _op("__sub__")
+    __rsub__ = _op("__sub__", reflected=True)
+    __mul__ = _op("__mul__")
+    __rmul__ = _op("__mul__", reflected=True)
+    __truediv__ = _op("__truediv__")
+    __rtruediv__ = _op("__truediv__", reflected=True)
+    del _op

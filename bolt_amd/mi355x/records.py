@@ -10,9 +10,16 @@ order), so such checks read the same against the mi355x mode.
 
 class RecordView(object):
 
-    def __init__(self, records, npartitions=1):
+    def __init__(self, records, npartitions=1, cached=False):
         self._records = list(records)
         self._npartitions = npartitions
+        self.is_cached = cached
+
+    def map(self, func):
+        return _ListView([func(kv) for kv in self._records])
+
+    def mapValues(self, func):
+        return RecordView([(k, func(v)) for k, v in self._records], self._npartitions)
 
     def collect(self):
         return list(self._records)

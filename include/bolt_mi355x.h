@@ -59,6 +59,15 @@ extern "C" {
 #define BM_STAT_SUM 3    /* reduce(operator.add)  array.py:243-282, :381-395 */
 #define BM_STAT_MAX 4    /* reduce(numpy.maximum) array.py:397-411 (NaN propagates) */
 #define BM_STAT_MIN 5    /* reduce(numpy.minimum) array.py:413-427 (NaN propagates) */
+/* reduce(func) with a numpy ufunc, array.py:243-282 (treeReduce(func)) */
+#define BM_STAT_PROD 6   /* numpy.multiply / operator.mul (bool: logical and)   */
+#define BM_STAT_LAND 7   /* numpy.logical_and -> bool                           */
+#define BM_STAT_LOR 8    /* numpy.logical_or  -> bool                           */
+#define BM_STAT_BAND 9   /* numpy.bitwise_and / operator.and_ (int, bool)       */
+#define BM_STAT_BOR 10   /* numpy.bitwise_or  / operator.or_  (int, bool)       */
+#define BM_STAT_BXOR 11  /* numpy.bitwise_xor / operator.xor  (int, bool)       */
+#define BM_STAT_FMAX 12  /* numpy.fmax (NaN ignored unless all NaN)             */
+#define BM_STAT_FMIN 13  /* numpy.fmin                                          */
 
 /* Version of this ABI (BM_ABI_VERSION).  Host code refuses a mismatch. */
 int bm_abi_version(void);
@@ -154,13 +163,21 @@ int bm_record_gather(const void *src, void *dst, int64_t nrec, int64_t src_rec,
  * before StatCounter / treeReduce run (array.py:269, :321-323).
  *
  * Arithmetic: floating inputs and every mean/var/std accumulate in float64
- * (pivot-shifted sums per lane, Chan combination across lanes, waves,
- * blocks and chunks in a fixed order: deterministic) and round once to
- * out_dtype.  SUM over integer dtypes is modular in the input width
+ * (combined across lanes, waves, blocks and chunks in a fixed order:
+ * deterministic) and round once to out_dtype.  SUM over integer dtypes is modular in the input width
  * (numpy add of same-dtype arrays wraps: the reference's treeReduce(add));
  * SUM over BM_BOOL is logical OR (numpy bool add).  MAX / MIN compare in the
- * input dtype with numpy.maximum / numpy.minimum semantics (a NaN wins).
- * out_dtype: BM_F16/BM_F32/BM_F64 for MEAN/VAR/STD; in_dtype for SUM/MAX/MIN.
+ * input dtype with numpy.maximum / numpy.minimum semantics (a NaN wins),
+ * FMAX / FMIN with numpy.fmax / numpy.fmin (a NaN loses).  PROD over floats
+ * accumulates in float64, over integers is modular in the input width, over
+ * BM_BOOL is logical AND.  LAND / LOR test x != 0 and write BM_BOOL;
+ * BAND / BOR / BXOR act on the element bits (integer and bool dtypes only).
+ * out_dtype: BM_F16/BM_F32/BM_F64 for MEAN/VAR/STD and float SUM/PROD;
+ * BM_BOOL for LAND/LOR; in_dtype otherwise.
+ * var / std: batched Welford -- each lane reduces a batch of up to 32 values
+ * around a pivot drawn from the batch, merged by Chan's formula
+ * (statcounter.py:51-59, :85-96) -- so the relative error of M2 stays
+ * O(32 eps) whatever the offset or outliers of the data.
  * Population variance (M2/n), std = sqrt(var), as statcounter.py:119-130.
  */
 int bm_reduce_workspace_bytes(int stat, int in_dtype, int64_t O, int64_t R,
@@ -174,9 +191,9 @@ int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
  * Partial reduction state for the multi-GPU merge (the per-partition
  * StatCounter of array.py:321-322).  `state` receives, for O*I outputs:
  *   MEAN/VAR/STD: two float64 planes, mean[O*I] then M2[O*I] (count = R);
- *   SUM float:    one float64 plane (the sum);
- *   SUM int/bool: one uint64 plane (modular sum / OR);
- *   MAX / MIN:    one uint64 plane holding the element's bits.
+ *   SUM / PROD float: one float64 plane (the sum / product);
+ *   SUM / PROD int/bool, LAND / LOR / BAND / BOR / BXOR: one uint64 plane;
+ *   MAX / MIN / FMAX / FMIN: one uint64 plane holding the element's bits.
  * bm_reduce_state_bytes gives the state size in bytes.
  */
 int bm_reduce_state_bytes(int stat, int in_dtype, int64_t nout, size_t *bytes);
@@ -190,11 +207,66 @@ int bm_reduce_state(int stat, const void *src, int in_dtype, int64_t O,
  * -- the StatCounter.combine tree of statcounter.py:67-99 / treeReduce of
  * array.py:323, made deterministic -- and finalise into out[nout].
  * counts: host array of nparts record counts (parts with count 0 are
- * skipped).  nparts <= 64.
+ * skipped).  nparts <= 256.
  */
 int bm_reduce_combine(int stat, int in_dtype, const void *states,
                       const int64_t *counts, int nparts, int64_t nout,
                       void *out, int out_dtype, void *stream);
+
+/*
+ * ---------------------------------------------------------------------------
+ * Multi-GPU record exchange over RCCL (xGMI), one process per GPU.
+ *
+ * These replace the Spark shuffles that move records between executors:
+ *   keys_to_values' partitionBy + _rebuild   bolt/spark/chunk.py:251-261
+ *   unchunk's partitionBy (shuffle #2)       bolt/spark/chunk.py:179-191
+ * (and so the swap / transpose that run through them, array.py:716-808), and
+ * the driver-side merge of per-partition statistics partials
+ * (treeReduce of StatCounter.combine, array.py:321-323).
+ * RCCL is bound at run time (dlopen): the librccl already in the process
+ * (PyTorch-ROCm's) is reused, else the system librccl.so.1.  All transfers
+ * are stream-ordered on `stream`; no call blocks the host on the transfer.
+ * Buffers are device memory owned by the caller; sizes and offsets in BYTES.
+ */
+#define BM_COMM_ID_BYTES 128   /* sizeof(ncclUniqueId) */
+
+/* Rank 0 creates the communicator id (BM_COMM_ID_BYTES) and sends it to the
+ * other ranks out of band (bolt_amd sends it through the torch.distributed
+ * rendezvous store). */
+int bm_comm_unique_id(void *id, size_t bytes);
+
+/* Collective over `world` ranks: every rank calls it with the same id and
+ * its own rank, with its GPU current.  *comm receives an opaque handle. */
+int bm_comm_init(void **comm, int world, const void *id, int rank);
+
+/* Release a communicator (NULL is a no-op). */
+int bm_comm_destroy(void *comm);
+
+/* rank / world of a communicator and the path of the RCCL library in use
+ * (lib may be NULL). */
+int bm_comm_info(void *comm, int *rank, int *world, char *lib, size_t lib_bytes);
+
+/*
+ * bm_alltoallv -- block q of send (send_bytes[q] bytes at send_offs[q]) goes
+ * to rank q; block s of recv (recv_bytes[s] at recv_offs[s]) arrives from rank
+ * s.  One RCCL group of ncclSend / ncclRecv pairs, every peer at once (each
+ * ordered GPU pair has its own xGMI link), the self block included.  The
+ * multi-GPU swap's exchange step (pack -> bm_alltoallv -> unpack).  Arrays
+ * have `world` entries; send_bytes[q] must equal what rank q expects.
+ */
+int bm_alltoallv(void *comm, const void *send, const int64_t *send_bytes,
+                 const int64_t *send_offs, void *recv, const int64_t *recv_bytes,
+                 const int64_t *recv_offs, void *stream);
+
+/*
+ * bm_allgatherv -- rank s's send_bytes (its `send`) land at recv_offs[s] of
+ * every rank's recv (recv_bytes[s] = rank s's send_bytes).  Uniform sizes at
+ * packed offsets use ncclAllGather, others one group of point-to-point pairs.
+ * Statistics states before bm_reduce_combine, and output slabs of reductions
+ * that keep the sharded axis.
+ */
+int bm_allgatherv(void *comm, const void *send, int64_t send_bytes, void *recv,
+                  const int64_t *recv_bytes, const int64_t *recv_offs, void *stream);
 
 #ifdef __cplusplus
 }

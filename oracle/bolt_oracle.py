@@ -381,6 +381,35 @@ def transpose(rs, p):
     return _values_permute(out, [int(i) - split for i in px[split:]])
 
 
+def _isreshapeable(new, old):
+    """bolt/utils.py:174-191: same number of elements, else ValueError."""
+    if int(np.prod(new)) != int(np.prod(old)):
+        raise ValueError("Total size of new keys must remain unchanged")
+
+
+def keys_reshape(rs, new):
+    """Keys.reshape (shapes.py:40-64): every key re-raveled into the new key shape."""
+    new = tuple(int(v) for v in new)
+    old = tuple(rs.shape[:rs.split])
+    _isreshapeable(new, old)
+    if new == old:
+        return rs
+    recs = [(tuple(int(i) for i in np.unravel_index(np.ravel_multi_index(k, old), new)), v)
+            for k, v in rs.records()]
+    return RecSet([recs], new + tuple(rs.shape[rs.split:]), len(new), rs.dtype)
+
+
+def values_reshape(rs, new):
+    """Values.reshape (shapes.py:111-134): every record's value reshaped."""
+    new = tuple(int(v) for v in new)
+    old = tuple(rs.shape[rs.split:])
+    _isreshapeable(new, old)
+    if new == old:
+        return rs
+    recs = [(k, v.reshape(new)) for k, v in rs.records()]
+    return RecSet([recs], tuple(rs.shape[:rs.split]) + new, rs.split, rs.dtype)
+
+
 # ---------------------------------------------------------------- statistics
 class StatCounter(object):
     """statcounter.py:28-130 (Welford merge, Chan combine), in the record dtype."""

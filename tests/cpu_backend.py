@@ -12,6 +12,9 @@ with the same output-dtype and modular-integer rules as the kernels.
 import numpy as np
 
 STAT_MEAN, STAT_VAR, STAT_STD, STAT_SUM, STAT_MAX, STAT_MIN = range(6)
+STAT_PROD, STAT_LAND, STAT_LOR, STAT_BAND, STAT_BOR, STAT_BXOR, STAT_FMAX, STAT_FMIN = range(6, 14)
+_PICK = {STAT_MAX: np.maximum, STAT_MIN: np.minimum, STAT_FMAX: np.fmax, STAT_FMIN: np.fmin}
+_BITOP = {STAT_BAND: np.bitwise_and, STAT_BOR: np.bitwise_or, STAT_BXOR: np.bitwise_xor}
 _CODES = [np.bool_, np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64,
           np.int64, np.float16, np.float32, np.float64]
 
@@ -78,10 +81,20 @@ class CpuBackend(object):
     def _planes(self, stat, code, x):
         """x: (O, R, I) in the input dtype -> state planes (list of arrays (O*I,))."""
         dt = np.dtype(_CODES[code])
-        if stat in (STAT_MAX, STAT_MIN):
-            f = np.maximum if stat == STAT_MAX else np.minimum
-            r = f.reduce(x, axis=1).reshape(-1)
+        if stat in _PICK:
+            r = _PICK[stat].reduce(x, axis=1).reshape(-1)
             return [_bits64(r)]
+        if stat in (STAT_LAND, STAT_LOR) or (stat == STAT_PROD and dt == np.bool_):
+            f = np.all if stat != STAT_LOR else np.any
+            return [f(x != 0, axis=1).reshape(-1).astype(np.uint64)]
+        if stat in _BITOP:
+            if dt.kind == 'f':
+                raise ValueError("bitwise reduction of a float dtype")
+            return [_BITOP[stat].reduce(_bits64(x).reshape(x.shape), axis=1).reshape(-1)]
+        if stat == STAT_PROD:
+            if dt.kind in 'iu':
+                return [np.multiply.reduce(x.astype(np.int64).astype(np.uint64), axis=1).reshape(-1)]
+            return [x.astype(np.float64).prod(axis=1).reshape(-1)]
         if stat == STAT_SUM:
             if dt == np.bool_:
                 return [x.any(axis=1).reshape(-1).astype(np.uint64)]
@@ -97,10 +110,13 @@ class CpuBackend(object):
         dt = np.dtype(_CODES[code])
         odt = np.dtype(_CODES[out_code])
         o = _np(out).view(odt)
-        if stat in (STAT_MAX, STAT_MIN):
+        if stat in _PICK or stat in _BITOP:
             o[...] = _unbits64(planes[0], dt)
             return
-        if stat == STAT_SUM:
+        if stat in (STAT_LAND, STAT_LOR) or (stat == STAT_PROD and dt == np.bool_):
+            o[...] = planes[0] != 0
+            return
+        if stat in (STAT_SUM, STAT_PROD):
             if dt.kind in 'iub':
                 o[...] = planes[0].astype(dt) if dt != np.bool_ else planes[0] != 0
             else:
@@ -143,10 +159,24 @@ class CpuBackend(object):
             if c <= 0:
                 continue
             part = buf[p * per:(p + 1) * per]
-            if stat in (STAT_MAX, STAT_MIN):
-                f = np.maximum if stat == STAT_MAX else np.minimum
+            if stat in _PICK:
                 v = _unbits64(part[:nout * 8].view(np.uint64), dt)
-                acc_m = v.copy() if acc_m is None else f(acc_m, v)
+                acc_m = v.copy() if acc_m is None else _PICK[stat](acc_m, v)
+                continue
+            if stat in _BITOP or stat in (STAT_LAND, STAT_LOR) or stat == STAT_PROD:
+                u = part[:nout * 8].view(np.uint64)
+                if stat == STAT_PROD and dt.kind == 'f':
+                    u = u.view(np.float64)
+                if acc_m is None:
+                    acc_m = u.copy()
+                elif stat in _BITOP:
+                    acc_m = _BITOP[stat](acc_m, u)
+                elif stat == STAT_LOR:
+                    acc_m = acc_m | u
+                elif stat == STAT_LAND or dt == np.bool_:
+                    acc_m = acc_m & u
+                else:
+                    acc_m = acc_m * u
                 continue
             if stat == STAT_SUM:
                 if dt.kind in 'iub':
@@ -165,8 +195,10 @@ class CpuBackend(object):
                 m = m + d * (c / tot)
                 q = q + qb + d * d * (n * c / tot)
                 n = tot
-        if stat in (STAT_MAX, STAT_MIN):
+        if stat in _PICK:
             planes = [_bits64(acc_m)]
+        elif stat in _BITOP or stat in (STAT_LAND, STAT_LOR) or stat == STAT_PROD:
+            planes = [acc_m]
         elif stat == STAT_SUM:
             planes = [acc_u] if dt.kind in 'iub' else [acc_f]
         else:

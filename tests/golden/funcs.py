@@ -5,6 +5,8 @@ tensor (the mi355x mode, whose user functions see device tensors); EXACT says
 whether the two agree bit for bit (elementwise IEEE arithmetic) or only to
 rounding (reductions, whose summation order differs).
 """
+import operator
+
 import numpy as np
 
 
@@ -70,3 +72,17 @@ FUNCS = {
 
 EXACT = {"double", "affine", "square", "crop_last", "dup_last", "flip_last", "to_f64", "first_row", "shrink0",
          "ones22", "tile12", "arr1", "arr0", "keyed"}
+
+# binary functions of the reduce golden cases (array.py:243-282): numpy ufuncs
+# and operator spellings run as one device reduction; the lambdas take the
+# generic path (a pairwise tree of the function on device tensors)
+RFUNCS = {
+    "add": operator.add, "np_add": np.add, "multiply": np.multiply, "mul": operator.mul,
+    "maximum": np.maximum, "minimum": np.minimum, "fmax": np.fmax, "fmin": np.fmin,
+    "logical_and": np.logical_and, "logical_or": np.logical_or,
+    "bitwise_and": np.bitwise_and, "bitwise_or": np.bitwise_or, "bitwise_xor": np.bitwise_xor,
+    "and_": operator.and_, "or_": operator.or_, "xor": operator.xor,
+    "lam_add": lambda a, b: a + b,
+    "lam_absadd": lambda a, b: abs(a) + abs(b),
+    "lam_mul": lambda a, b: a * b,
+}

@@ -16,7 +16,17 @@ def make_input(spec):
     if kind == "arange":
         return np.arange(n).astype(dtype).reshape(shape)
     if kind == "normal":
-        return rng.standard_normal(shape).astype(dtype)
+        x = rng.standard_normal(shape)
+        if "shift" in spec:  # offset data: shift + N(0,1), e.g. 1e6 + N(0,1)
+            x = spec["shift"] + x
+        if "outlier" in spec:  # value at index 0 of one axis, e.g. x[:, 0] = 100
+            ax, v = spec["outlier"]
+            idx = [slice(None)] * len(shape)
+            idx[ax] = 0
+            x[tuple(idx)] = v
+        if "nan_every" in spec:  # NaNs at every k-th element (fmax / fmin / maximum cases)
+            x.reshape(-1)[::spec["nan_every"]] = np.nan
+        return x.astype(dtype)
     if kind == "imaging":  # 1000 + 50 N(0,1): SURVEY.md 8(d) C2
         return (1000 + 50 * rng.standard_normal(shape)).astype(dtype)
     if kind == "bits":  # random bit patterns (NaN payloads included)

@@ -683,11 +683,122 @@ def gen_functional():
                 add(case, out=r.toarray())
 
 
+def gen_stats_numerics():
+    """float64 statistics where a pivot-shifted sum loses digits: an outlier at
+    index 0 of the reduced axis, and data offset far from zero (1e6 + N(0,1)),
+    reduced over a value axis (device rows kernel) and over the key axis
+    (device column kernel); float32 at a 1e3 offset.  n = 10,000."""
+    inputs = [
+        (spec((4, 10000), "float64", "normal", 70, outlier=[1, 100.0]), (0,), 1),
+        (spec((10000, 4), "float64", "normal", 71, outlier=[0, 100.0]), (0,), 0),
+        (spec((4, 10000), "float64", "normal", 72, shift=1e6), (0,), 1),
+        (spec((10000, 4), "float64", "normal", 73, shift=1e6), (0,), 0),
+        (spec((4, 10000), "float32", "normal", 74, shift=1e3), (0,), 1),
+        (spec((10000, 4), "float32", "normal", 75, outlier=[0, 100.0]), (0,), 0),
+        (spec((20, 500, 3), "float64", "normal", 76, shift=1e6), (0, 1), (0, 1)),
+    ]
+    for s, kaxis, red in inputs:
+        x = make_input(s)
+        for npart in (2, 8):
+            b = bolt.array(x, sc, axis=kaxis, npartitions=npart)
+            for name in ("mean", "var", "std"):
+                for ax in (red, None):
+                    case = {"op": "stat", "input": s, "axis": list(kaxis), "npartitions": npart,
+                            "name": name, "reduce_axis": list(ax) if isinstance(ax, tuple) else ax,
+                            "keepdims": False, "numerics": True}
+                    r = getattr(b, name)(axis=ax)
+                    case["result_type"] = type(r).__name__
+                    case["result_dtype"] = str(np.asarray(r).dtype)
+                    add(case, out=np.asarray(r))
+
+
+def gen_reshape():
+    """Keys.reshape / Values.reshape (shapes.py:40-64, :111-134), mirroring
+    test_spark_shaping.py:27-84 plus larger and multi-partition cases."""
+    x = spec((2, 3, 4))
+    y = spec((6, 4, 5), "float32", "normal", 80)
+    z = spec((8, 3, 2, 5), "uint16", "ints", 81)
+    items = [
+        (x, (0, 1), "keys", (3, 2), None), (x, (0,), "keys", (2, 1), None), (x, (0,), "keys", (2,), None),
+        (x, (0, 1), "keys", (2, 3), None), (x, (0, 1), "keys", (2, 3, 4), None),
+        (x, (0,), "values", (4, 3), None), (x, (0, 1), "values", (1, 4), None), (x, (0, 1), "values", (4,), None),
+        (x, (0,), "values", (3, 4), None), (x, (0, 1), "values", (2, 3, 4), None),
+        (y, (0, 1), "keys", (24,), 3), (y, (0, 1), "keys", (4, 6), 5), (y, (0, 1), "keys", (2, 2, 6), None),
+        (y, (0,), "keys", (3, 2), 2), (y, (0,), "values", (5, 4), 2), (y, (0,), "values", (20,), 4),
+        (y, (0,), "values", (2, 10), None), (y, (0, 1), "values", (5, 1), 3), (y, (0,), "values", (3, 7), None),
+        (z, (0, 1), "keys", (4, 6), 4), (z, (0, 1, 2), "keys", (48,), 3), (z, (0,), "values", (6, 5), 3),
+        (z, (0, 1), "values", (10,), 2), (z, (0, 1), "keys", (25,), None),
+    ]
+    for s, ax, which, new, npart in items:
+        xx = make_input(s)
+        b = bolt.array(xx, sc, axis=ax, npartitions=npart)
+        case = {"op": "reshape", "input": s, "axis": list(ax), "npartitions": npart, "which": which,
+                "new": list(new)}
+        r = run(lambda: getattr(b, which).reshape(new), case)
+        if r is None:
+            add(case)
+            continue
+        case.update(shape=list(r.shape), split=r.split)
+        add(case, out=r.toarray())
+    # varargs spelling: b.keys.reshape(3, 2)
+    xx = make_input(x)
+    b = bolt.array(xx, sc, axis=(0, 1))
+    r = b.keys.reshape(3, 2)
+    add({"op": "reshape", "input": x, "axis": [0, 1], "npartitions": None, "which": "keys", "new": [3, 2],
+         "varargs": True, "shape": list(r.shape), "split": r.split}, out=r.toarray())
+
+
+def gen_reduce():
+    """reduce(func, axis, keepdims) with numpy ufuncs, operator functions and
+    plain lambdas (array.py:243-282; test_spark_functional.py:31-48)."""
+    from funcs import RFUNCS
+    ia = spec((4, 3, 5))
+    f32 = spec((6, 4, 5), "float32", "normal", 90)
+    fnan = spec((5, 4, 3), "float64", "normal", 91, nan_every=7)
+    u8 = spec((7, 3, 4), "uint8", "ints", 92)
+    i16 = spec((6, 5), "int16", "ints", 93)
+    bb = spec((6, 5), "bool", "bool", 94)
+    one = spec((1, 4, 5), "float32", "normal", 95)
+    rep = spec((10, 10, 10))  # test_spark_functional.py:34-36 style (arange)
+    table = [
+        (ia, ["add", "np_add", "multiply", "mul", "maximum", "minimum", "fmax", "logical_and", "logical_or",
+              "bitwise_and", "bitwise_or", "bitwise_xor", "and_", "or_", "xor", "lam_add", "lam_absadd", "lam_mul"]),
+        (f32, ["add", "multiply", "maximum", "fmin", "logical_and", "logical_or", "bitwise_and", "lam_add",
+               "lam_absadd"]),
+        (fnan, ["maximum", "minimum", "fmax", "fmin", "add", "logical_and"]),
+        (u8, ["add", "multiply", "bitwise_and", "bitwise_or", "bitwise_xor", "maximum", "logical_or", "lam_mul"]),
+        (i16, ["multiply", "bitwise_xor", "fmin", "lam_add"]),
+        (bb, ["add", "multiply", "logical_and", "logical_or", "bitwise_xor", "maximum", "lam_add"]),
+        (one, ["add", "logical_and", "bitwise_and", "lam_absadd"]),
+        (rep, ["add", "maximum", "lam_add"]),
+    ]
+    for s, names in table:
+        x = make_input(s)
+        nd = len(s["shape"])
+        axes_list = [(0,), (1,), (0, 1)] + ([(0, 2), (0, 1, 2)] if nd == 3 else [])
+        for kax in ((0,), (0, 1)):
+            for npart in (None, 3):
+                b = bolt.array(x, sc, axis=kax, npartitions=npart)
+                for name in names:
+                    for ax in axes_list:
+                        for keep in ((False, True) if ax == (0,) else (False,)):
+                            case = {"op": "reduce", "input": s, "axis": list(kax), "npartitions": npart,
+                                    "func": name, "reduce_axis": list(ax), "keepdims": keep}
+                            r = run(lambda: b.reduce(RFUNCS[name], axis=ax, keepdims=keep), case)
+                            if r is None:
+                                add(case)
+                                continue
+                            case["result_type"] = type(r).__name__
+                            a = np.asarray(r.toarray() if hasattr(r, "toarray") else r)
+                            case["result_dtype"] = str(a.dtype)
+                            add(case, out=a)
+
+
 if __name__ == "__main__":
     sc = FakeContext(2)
     for g in (gen_construct, gen_swap, gen_transpose, gen_chunk, gen_moves, gen_getplan, gen_stats,
               gen_stat_errors, gen_getitem, gen_concatenate, gen_chunk_map,
-              gen_functional):
+              gen_functional, gen_stats_numerics, gen_reshape, gen_reduce):
         try:
             g()
         except Exception:

@@ -69,19 +69,29 @@ def truth_stat(x, name, axis):
     return var if name == "var" else np.sqrt(var)
 
 
-def stat_close(got, ref, truth, out_dtype, x):
+def stat_close(got, ref, truth, out_dtype, x, name="mean"):
     """The parity rule of SURVEY.md 8(c): |got-ref| <= rtol*|ref| + rtol*scale, with
-    rtol 1e-6 (float32/float16 outputs) / 1e-12 (float64); a result that is at least
-    as close to the float128 truth as the reference's also passes (the reference
-    accumulates float32 statistics in float32, order-dependently)."""
+    rtol 1e-6 (float32/float16 outputs) / 1e-12 (float64).  The scale has the units
+    of the statistic: max|x| for mean and sum, the reference's own variance
+    magnitude for var (its square root for std) -- never max|x| for var/std, which
+    would relax the bar on offset data.  A result that is at least as close to the
+    float128 truth as the reference's also passes (the reference accumulates
+    float32 statistics in float32, order-dependently)."""
     got = np.asarray(got, dtype=np.longdouble)
     ref = np.asarray(ref, dtype=np.longdouble)
     truth = np.asarray(truth, dtype=np.longdouble).reshape(ref.shape)
     rtol = 1e-12 if np.dtype(out_dtype) == np.float64 else 1e-6
     if np.dtype(out_dtype) == np.float16:
         rtol = 1e-3
-    scale = max(float(np.max(np.abs(np.asarray(x, dtype=np.longdouble)))) if np.size(x) else 0.0,
-                float(np.max(np.abs(ref))) if ref.size else 0.0, 1e-300)
+    finite = np.abs(ref[np.isfinite(ref)]) if ref.size else ref
+    if name in ("var", "std", "variance", "stdev"):
+        # per output: its own magnitude; a zero variance must come out (near) zero
+        scale = np.abs(ref) + np.finfo(out_dtype).eps * (float(np.max(finite)) if finite.size else 0.0)
+    else:
+        xa = np.abs(np.asarray(x, dtype=np.longdouble))
+        xa = xa[np.isfinite(xa)]
+        scale = max(float(np.max(xa)) if xa.size else 0.0,
+                    float(np.max(finite)) if finite.size else 0.0, 1e-300)
     ok1 = np.abs(got - ref) <= rtol * np.abs(ref) + rtol * scale
     eps = np.finfo(out_dtype).eps if np.dtype(out_dtype).kind == 'f' else 0
     ok2 = np.abs(got - truth) <= np.abs(ref - truth) + 2 * eps * np.abs(truth) + eps * rtol * scale
@@ -102,3 +112,31 @@ def index_arg(enc):
     if "tuple" in enc:
         return tuple(_dec_item(i) for i in enc["tuple"])
     return _dec_item(enc["item"])
+
+
+def truth_reduce(x, func_name, axis):
+    """float128 truth of a float reduce (sum / product) over ``axis``, or None."""
+    ax = tuple(axis)
+    v = np.asarray(x, dtype=np.longdouble)
+    if func_name in ("add", "np_add", "lam_add"):
+        return v.sum(axis=ax)
+    if func_name in ("multiply", "mul", "lam_mul"):
+        return v.prod(axis=ax)
+    if func_name == "lam_absadd":
+        return np.abs(v).sum(axis=ax)
+    return None
+
+
+def reduce_close(got, want, x, func_name, axis):
+    """Reduce parity: bit-exact for integer / bool results and for the selecting
+    ufuncs (maximum, minimum, fmax, fmin); floating sums and products by
+    stat_close's rule against their float128 truth (the reference accumulates
+    in the record dtype, in its treeReduce order)."""
+    got = np.asarray(got)
+    want = np.asarray(want)
+    if got.dtype != want.dtype or got.shape != want.shape:
+        return False
+    truth = truth_reduce(x, func_name, axis)
+    if want.dtype.kind != 'f' or truth is None:
+        return got.tobytes() == want.tobytes()
+    return stat_close(got, want, truth, want.dtype, x, "sum")

@@ -217,7 +217,7 @@ def test_stats_dtypes(bctx):
     assert m.dtype == np.float32 and m.shape == (16, 8)
     assert np.allclose(m, x.astype(np.float64).mean(0), rtol=1e-6)
     s = b.std(axis=0)
-    assert np.allclose(s, x.astype(np.float64).std(0), rtol=1e-5)
+    assert np.allclose(s, x.astype(np.float64).std(0), rtol=1e-6)
     u = rng.integers(0, 65536, size=(50, 8, 8)).astype(np.uint16)
     bu = bolt.array(u, bctx)
     v = bu.var(axis=0)

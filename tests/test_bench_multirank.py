@@ -63,10 +63,10 @@ def _body(rank, world):
             s = b.swap((0,), (0, 1))
             assert np.asarray(s.toarray()).tobytes() == np.ascontiguousarray(full.transpose(1, 2, 0)).tobytes()
             assert np.allclose(results["mean"], x.mean(0), rtol=1e-6)
-            assert np.allclose(results["std"], x.std(0), rtol=1e-5)
+            assert np.allclose(results["std"], x.std(0), rtol=1e-6)
         elif cfg == "target64":
             assert np.allclose(results["mean"], x.mean(0), rtol=1e-6)
-            assert np.allclose(results["std"], x.std(0), rtol=1e-5)
+            assert np.allclose(results["std"], x.std(0), rtol=1e-6)
             assert np.asarray(results["swap"].toarray()).tobytes() == \
                 np.ascontiguousarray(full.transpose(1, 2, 0, 3)).tobytes()
         elif cfg == "C3":

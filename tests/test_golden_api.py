@@ -152,7 +152,7 @@ def test_stat(case, bctx):
         assert np.asarray(got).tobytes() == want.tobytes()
     else:
         truth = G.truth_stat(x, case["name"], ax)
-        assert G.stat_close(got, want, truth, want.dtype, x)
+        assert G.stat_close(got, want, truth, want.dtype, x, case["name"])
 
 
 @pytest.mark.parametrize("case", G.cases("getitem"), ids=G.case_id)
@@ -301,3 +301,36 @@ def test_filter(case, bctx):
     assert list(r.shape) == case["shape"] and r.split == case["split"]
     if case["shape"] != [0]:
         assert r.toarray().tobytes() == G.arr(case, "out").tobytes()
+
+
+@pytest.mark.parametrize("case", G.cases("reduce"), ids=G.case_id)
+def test_reduce(case, bctx):
+    from funcs import RFUNCS
+    x, b = _b(case, bctx, case["npartitions"])
+    ax = tuple(case["reduce_axis"])
+    f = RFUNCS[case["func"]]
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            b.reduce(f, axis=ax, keepdims=case["keepdims"])
+        assert type(e.value).__name__ == case["raises"]
+        return
+    got = b.reduce(f, axis=ax, keepdims=case["keepdims"])
+    assert type(got).__name__ == case["result_type"]
+    a = np.asarray(got.toarray() if hasattr(got, "toarray") else got)
+    assert str(a.dtype) == case["result_dtype"]
+    assert G.reduce_close(a, G.arr(case, "out"), x, case["func"], ax)
+
+
+@pytest.mark.parametrize("case", G.cases("reshape"), ids=G.case_id)
+def test_reshape(case, bctx):
+    x, b = _b(case, bctx, case["npartitions"])
+    shp = getattr(b, case["which"])
+    new = tuple(case["new"])
+    if "raises" in case:
+        with pytest.raises(Exception) as e:
+            shp.reshape(new)
+        assert type(e.value).__name__ == case["raises"]
+        return
+    r = shp.reshape(*new) if case.get("varargs") else shp.reshape(new)
+    assert list(r.shape) == case["shape"] and r.split == case["split"]
+    assert r.toarray().tobytes() == G.arr(case, "out").tobytes()

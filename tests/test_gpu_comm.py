@@ -1,0 +1,99 @@
+"""The RCCL layer of libbolt_mi355x (include/bolt_mi355x.h, bm_comm.hip) on one GPU.
+
+A world-1 communicator drives every entry point: the id, init, info, the
+all-to-all (self block through an RCCL send/recv pair, sync and on the
+context's RCCL stream with event fences, as the pipelined swap uses it), the
+all-gather in both its ncclAllGather form and its point-to-point form, and
+destroy.  The multi-rank logic around these calls (block sizes, offsets,
+stages) is exercised by tests/test_dist_gloo.py over gloo; RCCL cannot put
+two ranks on one GPU, so N > 1 over RCCL runs in the driver's 8-GPU bench.
+Reference site replaced: bolt/spark/chunk.py:251-261 (shuffle #1).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from bolt_amd.mi355x import _lib
+from bolt_amd.mi355x import dist as D
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    lib = _lib.load()
+    uid = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+    _lib.check(lib.bm_comm_unique_id(uid, _lib.COMM_ID_BYTES), "bm_comm_unique_id")
+    c = ctypes.c_void_p()
+    _lib.check(lib.bm_comm_init(ctypes.byref(c), 1, uid, 0), "bm_comm_init")
+    yield c.value
+    _lib.check(lib.bm_comm_destroy(c.value), "bm_comm_destroy")
+
+
+class _Ctx(object):
+    """The attributes of MI355XContext the exchange helpers read."""
+
+    def __init__(self, comm):
+        import torch
+        self.comm = comm
+        self.comm_stream = torch.cuda.Stream()
+        self.rank, self.world_size = 0, 1
+
+
+def test_info_and_errors(comm):
+    lib = _lib.load()
+    rank, world = ctypes.c_int(-1), ctypes.c_int(-1)
+    where = ctypes.create_string_buffer(512)
+    _lib.check(lib.bm_comm_info(comm, ctypes.byref(rank), ctypes.byref(world), where, 512), "bm_comm_info")
+    assert (rank.value, world.value) == (0, 1)
+    assert b"rccl" in where.value.lower()
+    assert lib.bm_comm_unique_id(ctypes.create_string_buffer(8), 8) == -1  # BM_E_ARG
+    bad = _lib.i64_array([-1])
+    assert lib.bm_alltoallv(comm, None, bad, _lib.i64_array([0]), None, _lib.i64_array([0]),
+                            _lib.i64_array([0]), None) == -1
+
+
+@pytest.mark.parametrize("nbytes", [1, 4096, 37 << 20])
+def test_alltoallv_self(comm, nbytes):
+    import torch
+    ctx = _Ctx(comm)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
+    got = D._rccl_all_to_all(ctx, src, [nbytes], [nbytes], async_op=False)
+    torch.cuda.synchronize()
+    assert torch.equal(got, src)
+    got2, work = D._rccl_all_to_all(ctx, src, [nbytes], [nbytes], async_op=True)
+    work.wait()
+    assert torch.equal(got2, src)
+
+
+def test_allgatherv_both_forms(comm):
+    import torch
+    lib = _lib.load()
+    src = torch.arange(1000, dtype=torch.int32, device="cuda").view(torch.uint8)
+    n = src.numel()
+    ctx = _Ctx(comm)
+    out = D._rccl_all_gather(ctx, src, [n])  # uniform -> ncclAllGather
+    torch.cuda.synchronize()
+    assert torch.equal(out, src)
+    # a non-packed offset takes the point-to-point group
+    recv = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.bm_allgatherv(comm, src.data_ptr(), n, recv.data_ptr(), _lib.i64_array([n]),
+                                 _lib.i64_array([64]), torch.cuda.current_stream().cuda_stream), "bm_allgatherv")
+    torch.cuda.synchronize()
+    assert torch.equal(recv[64:], src) and int(recv[:64].sum()) == 0
+
+
+def test_exchange_helpers_with_a_comm(comm):
+    """all_to_all_bytes / all_gather_bytes take the RCCL route when the context
+    has a communicator (world 1: the pipelined swap's single peer is itself)."""
+    import torch
+    ctx = _Ctx(comm)
+    x = torch.from_numpy(np.arange(4096, dtype=np.int64)).cuda().view(torch.uint8)
+    recv, work = D.all_to_all_bytes(ctx, x, [x.numel()], [x.numel()], 8, async_op=True)
+    work.wait()
+    assert torch.equal(recv, x)

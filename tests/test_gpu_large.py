@@ -1,15 +1,21 @@
-"""Parity at the BASELINE.json sizes (GPU only), through size-independent properties.
+"""Parity at the BASELINE.json sizes (GPU only), bit for bit and in full.
 
-The oracle cannot run at 2-69 GB, so full-size checks use properties:
-  * swap / transpose round trips are the identity, bit for bit;
-  * thousands of random positions of the result equal the input at the
-    permuted coordinates (checked on the host from the input's bytes);
-  * chunk -> unchunk is the identity; a padded chunking keeps every record's
-    chunk cores exact at sampled positions;
-  * statistics agree with float64 sums taken with torch on the device (an
-    independent float64 reference for the floating-point kernels) within the
-    stated tolerance.
-Inputs are generated in HBM; every test frees its buffers.
+The oracle cannot run at 2-69 GB, so every output is compared, byte for byte
+and over its WHOLE extent, with an independent reference built on the same
+device by torch from the same input bytes:
+  * swap / transpose: ``x.permute(perm).contiguous()`` (viewed as integers,
+    so NaN payloads compare bitwise);
+  * chunk / keys_to_values / values_to_keys: the packed chunk layout rebuilt
+    with torch slicing from the reference's own slice rule
+    (chunk.py:574-618: chunk j of an axis is [j s - (j>0) p, j s + s + p)
+    clipped; records hold their chunks back to back in chunk-id order, each a
+    dense box), independent of plan.ChunkGeometry and the record-map kernels;
+  * statistics agree with float64 sums taken with torch on the device within
+    the stated tolerance.
+Configs: C2 swap, C3 swap and .T, C4 uint16 swap / .T / chunk('150'), C5 .T,
+transpose(2,0,4,1,3) and chunk((16,16), padding=2) with its k2v / v2k, the
+64 GiB target swap.  Inputs are generated in HBM; every test frees its
+buffers (the target's working set -- input, swap, reference -- is 206 GB).
 """
 import gc
 
@@ -19,6 +25,8 @@ import pytest
 import bolt_amd as bolt
 
 pytestmark = pytest.mark.gpu
+
+_INT = {1: "uint8", 2: "int16", 4: "int32", 8: "int64"}
 
 
 @pytest.fixture(autouse=True)
@@ -40,23 +48,25 @@ def _shard(ctx, shape, dtype, split, seed):
     return bolt.ConstructMI355X.fromshards(raw, shape, context=ctx, split=split, dtype=dtype), raw
 
 
-def _sample_check(src_raw, shape, dtype, out, perm, nsamp=4096, seed=0):
-    """out = x.transpose(perm): compare nsamp random output positions with the input."""
+def _ints(buf, es):
     import torch
-    rng = np.random.default_rng(seed)
+    return buf.view(getattr(torch, _INT[es]))
+
+
+def _full_check(raw, shape, dtype, out, perm):
+    """out = x.transpose(perm), every element, against torch's permute."""
+    import torch
     es = np.dtype(dtype).itemsize
-    oshape = tuple(shape[p] for p in perm)
-    idx = [rng.integers(0, d, nsamp) for d in oshape]
-    in_idx = [None] * len(shape)
-    for k, p in enumerate(perm):
-        in_idx[p] = idx[k]
-    lin_out = np.ravel_multi_index(idx, oshape)
-    lin_in = np.ravel_multi_index(in_idx, shape)
-    x = src_raw.view(torch.uint8).reshape(-1, es)
-    y = out._data.reshape(-1, es)
-    a = x[torch.from_numpy(lin_in).cuda()].cpu().numpy()
-    b = y[torch.from_numpy(lin_out).cuda()].cpu().numpy()
-    assert np.array_equal(a, b)
+    want = _ints(raw, es).reshape(shape).permute(*perm).contiguous().reshape(-1)
+    assert out._data.numel() == want.numel() * es
+    assert torch.equal(_ints(out._data, es), want)
+    del want
+
+
+def _clear():
+    import torch
+    gc.collect()
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("cfg", [
@@ -73,7 +83,7 @@ def test_swap_full_size(gpu_ctx, cfg):
     from bolt_amd.mi355x.plan import swap_perm
     perm, nsplit = swap_perm(len(shape), split, kax, vax)
     assert s.shape == tuple(shape[p] for p in perm) and s.split == nsplit
-    _sample_check(raw, shape, dtype, s, perm)
+    _full_check(raw, shape, dtype, s, perm)
     # undo the swap with the inverse permutation: bit-exact identity
     inv = list(np.argsort(perm))
     back = s.transpose(inv)
@@ -81,40 +91,85 @@ def test_swap_full_size(gpu_ctx, cfg):
     del s, back
 
 
-def test_transpose_full_size_c3_c5(gpu_ctx):
+@pytest.mark.parametrize("cfg", [
+    ((4096, 256, 256, 32), np.float32, 2, (3, 2, 1, 0)),        # C3 .T
+    ((64,) * 5, np.float64, 3, (4, 3, 2, 1, 0)),                # C5 .T
+    ((64,) * 5, np.float64, 3, (2, 0, 4, 1, 3)),                # C5 transpose(2,0,4,1,3)
+    ((10000, 1024, 1024), np.uint16, 1, (2, 1, 0)),             # C4 .T: packed-word tiles
+    ((2000, 1024, 2048), np.uint8, 1, (2, 1, 0)),               # uint8 .T
+], ids=["C3_T", "C5_T", "C5_20413", "C4_T", "u8_T"])
+def test_transpose_full_size(gpu_ctx, cfg):
     import torch
-    for shape, dtype, split, perm in [((4096, 256, 256, 32), np.float32, 2, (3, 2, 1, 0)),
-                                      ((64,) * 5, np.float64, 3, (4, 3, 2, 1, 0)),
-                                      ((64,) * 5, np.float64, 3, (2, 0, 4, 1, 3)),
-                                      # C4's uint16 reversed: packed-word tiles (k_transpose_pk)
-                                      ((10000, 1024, 1024), np.uint16, 1, (2, 1, 0)),
-                                      ((2000, 1024, 2048), np.uint8, 1, (2, 1, 0))]:
-        b, raw = _shard(gpu_ctx, shape, dtype, split, 3)
-        t = b.transpose(perm)
-        _sample_check(raw, shape, dtype, t, perm)
-        back = t.transpose(list(np.argsort(perm)))
-        assert torch.equal(back._data, b._data)
-        del b, raw, t, back
-        gc.collect()
-        torch.cuda.empty_cache()
+    shape, dtype, split, perm = cfg
+    b, raw = _shard(gpu_ctx, shape, dtype, split, 3)
+    t = b.transpose(perm)
+    _full_check(raw, shape, dtype, t, perm)
+    back = t.transpose(list(np.argsort(perm)))
+    assert torch.equal(back._data, b._data)
+    del b, raw, t, back
 
 
-def test_chunk_round_trips_full_size(gpu_ctx):
+def _axis_slices(d, s, p):
+    """getslices (chunk.py:574-618) for one axis: [j s - (j>0) p, j s + s + p) clipped."""
+    out, j = [], 0
+    while j * s < d:
+        out.append(slice(max(0, j * s - (p if j else 0)), min(d, j * s + s + p)))
+        j += 1
+    return out
+
+
+def _packed_ref(rec, vshape, plan, pad):
+    """(records, *vshape) device tensor -> its packed chunk layout, by torch slicing."""
+    import torch
+    from itertools import product
+    sl = [_axis_slices(vshape[a], plan[a], pad[a]) for a in range(len(vshape))]
+    parts = [rec[(slice(None),) + tuple(c)].reshape(rec.shape[0], -1) for c in product(*sl)]
+    return torch.cat(parts, dim=1).reshape(-1)
+
+
+def test_chunk_c4_full_size(gpu_ctx):
     import torch
     b, raw = _shard(gpu_ctx, (10000, 1024, 1024), np.uint16, 1, 11)   # C4, size '150'
     c = b.chunk("150")
-    assert tuple(c.plan) == (73, 1024)
+    assert tuple(c.plan) == (73, 1024) and tuple(c.padding) == (0, 0)
+    want = _packed_ref(_ints(raw, 2).reshape(10000, 1024, 1024), (1024, 1024), (73, 1024), (0, 0))
+    assert torch.equal(_ints(c._packed, 2), want)
+    del want
     assert torch.equal(c.unchunk()._data, b._data)
-    del c, b, raw
-    gc.collect()
-    torch.cuda.empty_cache()
+
+
+def test_chunk_c5_full_size(gpu_ctx):
+    import torch
     b, raw = _shard(gpu_ctx, (64,) * 5, np.float64, 3, 12)            # C5, padded
+    x = _ints(raw, 8).reshape((64,) * 5)
     c = b.chunk((16, 16), padding=2)
+    want = _packed_ref(x.reshape(64 ** 3, 64, 64), (64, 64), (16, 16), (2, 2))
+    assert torch.equal(_ints(c._packed, 8), want)
+    del want
     assert torch.equal(c.unchunk()._data, b._data)
+    # keys_to_values((2,)): keys (k0, k1), values (k2, v0, v1), plan (64, 16, 16), padding (0, 2, 2)
     k = c.keys_to_values((2,))
-    assert torch.equal(k.unchunk()._data, b.swap((2,), ())._data)
+    assert tuple(k.plan) == (64, 16, 16) and tuple(k.padding) == (0, 2, 2)
+    want = _packed_ref(x.reshape(64 * 64, 64, 64, 64), (64, 64, 64), (64, 16, 16), (0, 2, 2))
+    assert torch.equal(_ints(k._packed, 8), want)
+    del want, k
+    _clear()
+    # values_to_keys((0,)): keys (k0, k1, k2, v0), values (v1,), plan (16,), padding (2,)
     v = c.values_to_keys((0,))
+    assert tuple(v.plan) == (16,) and tuple(v.padding) == (2,)
+    want = _packed_ref(x.reshape(64 ** 4, 64), (64,), (16,), (2,))
+    assert torch.equal(_ints(v._packed, 8), want)
+    del want
     assert torch.equal(v.unchunk()._data, b.swap((), (0,))._data)
+
+
+def test_target64_swap_full_size(gpu_ctx):
+    """The 64 GiB north_star array: float32 (8192, 256, 256, 32), split 2, swap((0,), (0,))."""
+    shape = (8192, 256, 256, 32)
+    b, raw = _shard(gpu_ctx, shape, np.float32, 2, 21)
+    s = b.swap((0,), (0,))
+    assert s.shape == (256, 256, 8192, 32) and s.split == 2
+    _full_check(raw, shape, np.float32, s, (1, 2, 0, 3))
 
 
 def test_stats_full_size_c2(gpu_ctx):

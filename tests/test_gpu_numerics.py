@@ -1,0 +1,97 @@
+"""float64 var/std accuracy of the device reductions on ill-conditioned data.
+
+The reference's StatCounter runs Welford per record (statcounter.py:51-59)
+and merges partitions by Chan's formula (:85-96).  bm_reduce keeps a Welford
+state per lane, built from batches of up to 32 values around a pivot drawn
+from the batch and shifted by the row's first element, so neither an outlier
+at the start of the reduced axis nor a large common offset costs digits.
+These cases size the reduction so that each output is ONE chunk of >= 10,000
+values (the case a single first-element pivot handles worst) and check every
+output against the float128 truth at the north_star rtol of 1e-12, pure
+relative (no absolute slack).  Parity pinned by the golden "numerics" stat
+fixtures (tests/golden, make_golden.gen_stats_numerics) at small sizes.
+"""
+import numpy as np
+import pytest
+
+import bolt_amd as bolt
+
+pytestmark = pytest.mark.gpu
+
+
+def _truth_rows(x):
+    v = x.astype(np.longdouble)
+    return v.var(axis=-1)
+
+
+def _check(got, truth, rtol):
+    got = np.asarray(got, dtype=np.longdouble)
+    err = np.abs(got - truth) / np.abs(truth)
+    assert float(err.max()) <= rtol, float(err.max())
+
+
+@pytest.mark.parametrize("kind", ["outlier", "offset", "outlier1e3"])
+def test_rows_single_chunk(gpu_ctx, kind):
+    # (8192, 10000): >= 8192 rows -> one chunk per row in the rows kernel
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((8192, 10000))
+    if kind == "outlier":
+        x[:, 0] = 100.0
+    elif kind == "outlier1e3":
+        x[:, 0] = 1e3
+    else:
+        x += 1e6
+    b = bolt.array(x, gpu_ctx, axis=(0,))
+    var = b.var(axis=1)
+    std = b.std(axis=1)
+    sel = rng.choice(x.shape[0], 256, replace=False)
+    t = _truth_rows(x[sel])
+    _check(np.asarray(var)[sel], t, 1e-12)
+    _check(np.asarray(std)[sel], np.sqrt(t), 1e-12)
+
+
+@pytest.mark.parametrize("kind", ["outlier", "offset"])
+def test_cols_single_chunk(gpu_ctx, kind):
+    # (2048, 10000, 2) reduced over axis 1: 2048 column tiles -> one chunk of
+    # 10,000 rows, 256 row phases per tile merged in LDS
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((2048, 10000, 2))
+    if kind == "outlier":
+        x[:, 0, :] = 100.0
+    else:
+        x += 1e6
+    b = bolt.array(x, gpu_ctx, axis=(0,))
+    var = np.asarray(b.var(axis=1))
+    sel = rng.choice(x.shape[0], 64, replace=False)
+    t = x[sel].astype(np.longdouble).var(axis=1)
+    _check(var[sel], t, 1e-12)
+
+
+@pytest.mark.parametrize("kind", ["outlier", "offset"])
+def test_key_axis_chunked(gpu_ctx, kind):
+    # variance over the key axis with few outputs: R split into chunks whose
+    # states are merged by the combine kernel around the shared pivot
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((200000, 8))
+    if kind == "outlier":
+        x[0, :] = 100.0
+    else:
+        x += 1e6
+    b = bolt.array(x, gpu_ctx, axis=(0,))
+    t = x.astype(np.longdouble).var(axis=0)
+    _check(b.var(axis=0), t, 1e-12)
+    _check(b.std(axis=0), np.sqrt(t), 1e-12)
+    tall = x.astype(np.longdouble).var()
+    _check(np.asarray(b.var()), tall, 1e-12)
+
+
+def test_float32_offset(gpu_ctx):
+    # float32 input, float64 accumulation, one rounding to float32
+    rng = np.random.default_rng(10)
+    x = (1e3 + rng.standard_normal((4096, 4000))).astype(np.float32)
+    b = bolt.array(x, gpu_ctx, axis=(0,))
+    v = np.asarray(b.var(axis=1))
+    assert v.dtype == np.float32
+    t = x.astype(np.longdouble).var(axis=1)
+    err = np.abs(v.astype(np.longdouble) - t) / t
+    assert float(err.max()) <= 1e-6
