@@ -2,6 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5|target64]
 
+The default run (C2 on one GPU) also times BASELINE.json's target -- swap +
+mean/std of a 64 GiB float32 (8192,256,256,32) array -- and reports it as the
+`target64` sub-record of the same JSON line (`value` stays C2's).
+
 One "step" = one pass of the hot path over one batch of synthetic input,
 resident in HBM before timing starts.  Default workload (BASELINE.json
 configs[1], "C2"): float32 (2000, 512, 512) time series per GPU, key = time
@@ -61,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-target64", action="store_true",
+                    help="skip the 64 GiB north_star sub-record of the default (C2, 1 GPU) run")
+    ap.add_argument("--target-steps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -282,156 +289,164 @@ def main():
     ctx = MI355XContext(device=dev)
     assert ctx.world_size == world
 
-    shape, dtype, split, desc = CONFIGS[args.config]
-    gshape = (shape[0] * world,) + tuple(shape[1:])
-    shard = synth_shard(torch, shape, dtype, dev, 1234 + rank)
-    b = bolt.ConstructMI355X.fromshards(shard, gshape, context=ctx, split=split, dtype=dtype)
-    del shard
-
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    ops = steps_of(args.config, b, world)
-    if args.pmc_child:  # profiled child of pmc_traffic(): the roofline op only, no output
-        for _ in range(args.warmup + args.steps):
-            r = ops[0][1]()
-            del r
-        torch.cuda.synchronize()
-        return
+    def measure(cfg, steps, warmup):
+        """One config's timed run -> its JSON line (without PMC traffic / CPU baseline)."""
+        shape, dtype, split, desc = CONFIGS[cfg]
+        gshape = (shape[0] * world,) + tuple(shape[1:])
+        shard = synth_shard(torch, shape, dtype, dev, 1234 + rank)
+        b = bolt.ConstructMI355X.fromshards(shard, gshape, context=ctx, split=split, dtype=dtype)
+        del shard
 
-    for _ in range(args.warmup):
-        for _, call, _ in ops:
-            r = call()
-            del r
-    barrier()
+        ops = steps_of(cfg, b, world)
+        if args.pmc_child:  # profiled child of pmc_traffic(): the roofline op only, no output
+            for _ in range(warmup + steps):
+                r = ops[0][1]()
+                del r
+            torch.cuda.synchronize()
+            return None
 
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    # hipEvents bracketing the permute kernel's own launch, on the stream it runs on
-    from bolt_amd.mi355x._ops import backend_for
-    be = backend_for(dev)
-    kev = []
-    # event pairs made before the timed region (one permute launch per swap on
-    # one GPU; the pipelined multi-GPU swap launches more and draws extra pairs)
-    kpool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-             for _ in range(args.steps)]
-    permute0 = be.permute
-    timing = {"on": False}
+        for _ in range(warmup):
+            for _, call, _ in ops:
+                r = call()
+                del r
+        barrier()
 
-    def timed_permute(*a, **k):
-        if not timing["on"]:
-            return permute0(*a, **k)
-        if len(kev) < len(kpool):
-            e0, e1 = kpool[len(kev)]
-        else:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        permute0(*a, **k)
-        e1.record(stream)
-        kev.append((e0, e1))
-    be.permute = timed_permute
-    from bolt_amd.mi355x import dist as bdist
-    if world > 1:
-        bdist.PROFILE = {}  # hipEvent pairs around pack / all_to_all / unpack
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        for k, (_, call, _) in enumerate(ops):
-            if k == 0:
-                if world > 1:
-                    ev[i][0].record(stream)
-                timing["on"] = True
-            r = call()
-            if k == 0:
-                timing["on"] = False
-                if world > 1:
-                    ev[i][1].record(stream)
-            del r
-    barrier()
-    elapsed = time.perf_counter() - t0
-    be.permute = permute0
-    phases = {}
-    if bdist.PROFILE is not None:
-        for k, evs in bdist.PROFILE.items():
-            phases[k] = float(np.mean([a.elapsed_time(z) for a, z in evs]))
-        bdist.PROFILE = None
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        # hipEvents bracketing the permute kernel's own launch, on the stream it runs on
+        from bolt_amd.mi355x._ops import backend_for
+        be = backend_for(dev)
+        kev = []
+        # event pairs made before the timed region (one permute launch per swap on
+        # one GPU; the pipelined multi-GPU swap launches more and draws extra pairs)
+        kpool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                 for _ in range(steps)]
+        permute0 = be.permute
+        timing = {"on": False}
 
-    # On one GPU the swap call is the one permute launch, so only the kernel's
-    # own event pair is recorded (each extra stream event adds a few us between
-    # the kernels); across GPUs the call's pair brackets the whole exchange.
-    kern_ms = float(np.mean([a.elapsed_time(z) for a, z in kev])) if kev else None
-    swap_ms = float(np.mean([a.elapsed_time(z) for a, z in ev])) if world > 1 else kern_ms
-    if kern_ms is None:  # (no permute launch in the op: the step's wall time bounds it)
-        kern_ms = swap_ms if swap_ms is not None else elapsed / args.steps * 1e3
-        swap_ms = kern_ms
-    per = {name: nb * world for name, _, nb in ops}
-    total = sum(per.values()) * args.steps
-    value = total / elapsed / 1e9
-    swap_bytes_rank = ops[0][2]
-    achieved = swap_bytes_rank / (kern_ms / 1e3) / 1e9
+        def timed_permute(*a, **k):
+            if not timing["on"]:
+                return permute0(*a, **k)
+            if len(kev) < len(kpool):
+                e0, e1 = kpool[len(kev)]
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            permute0(*a, **k)
+            e1.record(stream)
+            kev.append((e0, e1))
+        be.permute = timed_permute
+        from bolt_amd.mi355x import dist as bdist
+        if world > 1:
+            bdist.PROFILE = {}  # hipEvent pairs around pack / all_to_all / unpack
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            for k, (_, call, _) in enumerate(ops):
+                if k == 0:
+                    if world > 1:
+                        ev[i][0].record(stream)
+                    timing["on"] = True
+                r = call()
+                if k == 0:
+                    timing["on"] = False
+                    if world > 1:
+                        ev[i][1].record(stream)
+                del r
+        barrier()
+        elapsed = time.perf_counter() - t0
+        be.permute = permute0
+        phases = {}
+        if bdist.PROFILE is not None:
+            for k, evs in bdist.PROFILE.items():
+                phases[k] = float(np.mean([a.elapsed_time(z) for a, z in evs]))
+            bdist.PROFILE = None
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
 
-    line = {
-        "metric": "swap/transpose GB/s + stat-reduce GB/s, % of HBM/xGMI roofline, 1-8 GPUs",
-        "value": round(value, 2),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": {"float32": "f32", "float64": "f64", "uint16": "u16"}[np.dtype(dtype).name],
-        "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
-        "config": {"workload": desc, "global_shape": list(gshape), "split": split,
-                   "parallelism": "dp%d (records sharded on the leading key axis)" % world,
-                   "collectives": "RCCL via libbolt_mi355x (bm_alltoallv / bm_allgatherv)" if backend == "nccl" or world == 1
-                                  else "%s, host-staged (one-GPU rehearsal, not a measurement)" % backend,
-                   "bytes_per_step": {k: int(v) for k, v in per.items()}},
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "%s (bm_permute) for the %s" % (ROOFLINE_KERNEL[args.config], ops[0][0]) if world == 1 else
-                      "swap = pack + RCCL all_to_all + unpack (per rank)",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
+        # On one GPU the swap call is the one permute launch, so only the kernel's
+        # own event pair is recorded (each extra stream event adds a few us between
+        # the kernels); across GPUs the call's pair brackets the whole exchange.
+        kern_ms = float(np.mean([a.elapsed_time(z) for a, z in kev])) if kev else None
+        swap_ms = float(np.mean([a.elapsed_time(z) for a, z in ev])) if world > 1 else kern_ms
+        if kern_ms is None:  # (no permute launch in the op: the step's wall time bounds it)
+            kern_ms = swap_ms if swap_ms is not None else elapsed / steps * 1e3
+            swap_ms = kern_ms
+        per = {name: nb * world for name, _, nb in ops}
+        total = sum(per.values()) * steps
+        value = total / elapsed / 1e9
+        swap_bytes_rank = ops[0][2]
+        achieved = swap_bytes_rank / (kern_ms / 1e3) / 1e9
+
+        line = {
+            "metric": "swap/transpose GB/s + stat-reduce GB/s, % of HBM/xGMI roofline, 1-8 GPUs",
+            "value": round(value, 2),
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None,
-            "avg_ms": round(kern_ms, 4),
-            "swap_call_ms": round(swap_ms, 4),
-            "bytes_per_launch": int(swap_bytes_rank),
-        },
-    }
-    if world > 1:
-        G = world
-        n_rank = ops[0][2] / 2                        # bytes held per rank
-        payload = n_rank * (G - 1) / G                # bytes each rank sends to its peers
-        ex = phases.get("exchange")
-        if ex:  # the swap across GPUs: pipelined pack -> RCCL all-to-all -> unpack
-            line["roofline"].update({"kernel": "swap exchange per rank (k_transpose pack + RCCL "
-                                               "all_to_all + k_rowcopy unpack, pipelined)",
-                                     "achieved": round(2 * n_rank / (ex / 1e3) / 1e9, 1),
-                                     "avg_ms": round(ex, 4), "bytes_per_launch": int(2 * n_rank)})
-            line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
-        a2a = phases.get("exchange")
-        peak = (G - 1) * XGMI_LINK_GBPS
-        line["xgmi"] = {"op": "RCCL send/recv group (bm_alltoallv) inside the pipelined swap exchange "
-                              "(achieved = peer payload / whole exchange time: a lower bound)",
-                        "payload_bytes_per_rank": int(payload),
-                        "avg_ms": round(a2a, 4) if a2a else None,
-                        "achieved": round(payload / (a2a / 1e3) / 1e9, 1) if a2a else None,
-                        "peak": peak, "unit": "GB/s per rank (egress)",
-                        "frac": round(payload / (a2a / 1e3) / 1e9 / peak, 4) if a2a else None,
-                        "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
-    line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
-    line["roofline"]["measured_copy_peak"] = HBM_COPY_GBPS
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": {"float32": "f32", "float64": "f64", "uint16": "u16"}[np.dtype(dtype).name],
+            "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
+            "config": {"workload": desc, "global_shape": list(gshape), "split": split,
+                       "parallelism": "dp%d (records sharded on the leading key axis)" % world,
+                       "collectives": "RCCL via libbolt_mi355x (bm_alltoallv / bm_allgatherv)" if backend == "nccl" or world == 1
+                                      else "%s, host-staged (one-GPU rehearsal, not a measurement)" % backend,
+                       "bytes_per_step": {k: int(v) for k, v in per.items()}},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "%s (bm_permute) for the %s" % (ROOFLINE_KERNEL[cfg], ops[0][0]) if world == 1 else
+                          "swap = pack + RCCL all_to_all + unpack (per rank)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "avg_ms": round(kern_ms, 4),
+                "swap_call_ms": round(swap_ms, 4),
+                "bytes_per_launch": int(swap_bytes_rank),
+            },
+        }
+        if world > 1:
+            G = world
+            n_rank = ops[0][2] / 2                        # bytes held per rank
+            payload = n_rank * (G - 1) / G                # bytes each rank sends to its peers
+            ex = phases.get("exchange")
+            if ex:  # the swap across GPUs: pipelined pack -> RCCL all-to-all -> unpack
+                line["roofline"].update({"kernel": "swap exchange per rank (k_transpose pack + RCCL "
+                                                   "all_to_all + k_rowcopy unpack, pipelined)",
+                                         "achieved": round(2 * n_rank / (ex / 1e3) / 1e9, 1),
+                                         "avg_ms": round(ex, 4), "bytes_per_launch": int(2 * n_rank)})
+                line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
+            a2a = phases.get("exchange")
+            peak = (G - 1) * XGMI_LINK_GBPS
+            line["xgmi"] = {"op": "RCCL send/recv group (bm_alltoallv) inside the pipelined swap exchange "
+                                  "(achieved = peer payload / whole exchange time: a lower bound)",
+                            "payload_bytes_per_rank": int(payload),
+                            "avg_ms": round(a2a, 4) if a2a else None,
+                            "achieved": round(payload / (a2a / 1e3) / 1e9, 1) if a2a else None,
+                            "peak": peak, "unit": "GB/s per rank (egress)",
+                            "frac": round(payload / (a2a / 1e3) / 1e9 / peak, 4) if a2a else None,
+                            "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
+        line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
+        line["roofline"]["measured_copy_peak"] = HBM_COPY_GBPS
+        return line
+
+    line = measure(args.config, args.steps, args.warmup)
+    if line is None:
+        return
+    shape, dtype, split, desc = CONFIGS[args.config]
     if rank == 0 and world == 1 and not args.no_pmc:
         traffic, note = pmc_traffic(args.config)
         line["roofline"]["traffic"] = int(traffic) if traffic else None
@@ -439,6 +454,24 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rows = args.cpu_sample_rows or 2000
         line["cpu_baseline"] = cpu_baseline(args.config, shape, dtype, rows)
+    if world == 1 and args.config == "C2" and not args.no_target64:
+        # BASELINE.json's target sentence: swap and statistics of a 64 GiB
+        # float32 4-D array on one GPU at >= 60% of the HBM roofline
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        t = measure("target64", args.target_steps, 1)
+        sub = {"workload": CONFIGS["target64"][3], "value": t["value"], "unit": "GB/s",
+               "ms_per_step": t["ms_per_step"], "steps": t["steps"], "warmup": t["warmup"],
+               "global_shape": t["config"]["global_shape"], "bytes_per_step": t["config"]["bytes_per_step"],
+               "frac_of_hbm_peak": round(t["value"] / HBM_PEAK_GBPS, 4),
+               "target": "swap + mean/std of 64 GiB on 1 GPU at >= 0.60 of HBM (swap <= 28.6 ms)",
+               "roofline": t["roofline"]}
+        if not args.no_pmc:
+            traffic, note = pmc_traffic("target64")
+            sub["roofline"]["traffic"] = int(traffic) if traffic else None
+            sub["roofline"]["traffic_note"] = note
+        line["target64"] = sub
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

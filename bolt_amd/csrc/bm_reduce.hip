@@ -644,15 +644,23 @@ __global__ void __launch_bounds__(kThreads)
       }
     }
   }
+  // var / std: the rest of the row and the cross-lane merge run as sums
+  // around one wave-wide pivot C = lane 0's Welford mean (lane 0 holds 1/64
+  // of the main-loop data, so n (mean - C)^2 <= 64 M2 and S2 - S1^2/n loses
+  // at most ~6 bits): plain adds, no division per lane or per butterfly step
+  const double C = (MODE == M_MOM) ? __shfl(w.mean, 0) : 0.0;
+  double t1 = 0.0, t2 = 0.0;
   for (; j < r_hi; j += stride) {
     if (j + VEC <= r_hi) {
       T v[VEC];
       vload_nt<T, VEC>(row + j, v);
       if constexpr (MODE == M_MOM) {
-        double x[VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) x[k] = to_f64(v[k]);
-        w.add_batch<VEC>(x, P);
+        for (int k = 0; k < VEC; ++k) {
+          const double y = (to_f64(v[k]) - P) - C;
+          t1 += y;
+          t2 = fma(y, y, t2);
+        }
         continue;
       }
 #pragma unroll
@@ -663,8 +671,11 @@ __global__ void __launch_bounds__(kThreads)
       }
     } else {
       for (int64_t k = j; k < r_hi; ++k) {
-        if (MODE == M_MOM) w.add1(to_f64(row[k]) - P);
-        else if (MODE == M_MEAN) acc.add(to_f64(row[k]));
+        if (MODE == M_MOM) {
+          const double y = (to_f64(row[k]) - P) - C;
+          t1 += y;
+          t2 = fma(y, y, t2);
+        } else if (MODE == M_MEAN) acc.add(to_f64(row[k]));
         else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(row[k]));
         else us = bop<T, MODE>(us, belem<T, MODE>(row[k]));
       }
@@ -674,17 +685,21 @@ __global__ void __launch_bounds__(kThreads)
   // wave combination (butterfly, fixed order -> deterministic).  Both lanes
   // of a pair combine (lower lane, upper lane) in that order, so they hold
   // identical bits afterwards.  mean: shared pivot, the S1 sums simply add;
-  // var / std: Chan merges of the lanes' Welford states.
+  // var / std: each lane's Welford state as sums around C, which add.
   double m = facc_mode<MODE>() ? fs : acc.s1();
-  double n = w.n, wm = w.mean, wq = w.m2;
+  double wq = 0.0;
+  if constexpr (MODE == M_MOM) {
+    const double dm = w.mean - C;
+    const double s1 = w.n * dm;
+    m = s1 + t1;
+    wq = fma(s1, dm, w.m2) + t2;
+  }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     if (MODE == M_MOM) {
-      const double nb = __shfl_xor(n, off), mb = __shfl_xor(wm, off), qb = __shfl_xor(wq, off);
-      const bool up = (lane & off) != 0;
-      double na = up ? nb : n, ma = up ? mb : wm, qa = up ? qb : wq;
-      chan(na, ma, qa, up ? n : nb, up ? wm : mb, up ? wq : qb, true);
-      n = na; wm = ma; wq = qa;
+      const double mb = __shfl_xor(m, off), qb = __shfl_xor(wq, off);
+      m = (lane & off) ? (mb + m) : (m + mb);
+      wq = (lane & off) ? (qb + wq) : (wq + qb);
     } else if (MODE == M_MEAN || facc_mode<MODE>()) {
       const double mb = __shfl_xor(m, off);
       // lower lane combines (self, partner), upper lane (partner, self)
@@ -699,7 +714,9 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t e = (int64_t)o;
   const int64_t idx = sk.final_out ? e : (c * d.O + e);
   if constexpr (MODE == M_MOM) {
-    emit_mom(sk, idx, e, c, ntot, wm, wq, P);
+    // (S1, S2) around C -> mean - P and M2
+    const double q = fma(-m, m / ntot, wq);
+    emit_mom(sk, idx, e, c, ntot, C + m / ntot, q, P);
     return;
   }
   if (MODE == M_MEAN) m = mean_from_sums(ntot, acc.K, m);
