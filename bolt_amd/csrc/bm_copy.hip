@@ -66,6 +66,15 @@ constexpr int kThreads = 256;
 #ifndef BM_GEN_GRIDCAP
 #define BM_GEN_GRIDCAP 4096  // generic copies: grid-stride (uncapped measured -20% on reversed slices, r01_index2)
 #endif
+#ifndef BM_RC_SKEW
+#define BM_RC_SKEW 0  // rowcopy: diagonal row walk when the fastest row dim's source step is >= this many bytes (0 = off; A/B knob)
+#endif
+#ifndef BM_RC_SKEW_MAXB
+#define BM_RC_SKEW_MAXB 256  // ... and rows are at most this many bytes (longer rows already spread over L2 channels)
+#endif
+#ifndef BM_TR_SKEW
+#define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
+#endif
 #ifndef BM_FUSE
 #define BM_FUSE 1  // fuse short contiguous transpose axes with their continuation (A/B knob)
 #endif
@@ -426,7 +435,7 @@ bool fill_decomp(Decomp &d, const std::vector<Dim> &outer_to_inner) {
   const int n = (int)outer_to_inner.size();
   if (n > BM_MAXD) return false;
   d.n = n;
-  d.pad_ = 0;
+  d.skew = 0;
   for (int k = 0; k < n; ++k) {  // store innermost first
     const Dim &x = outer_to_inner[n - 1 - k];
     d.div[k] = make_fastdiv((uint64_t)x.n);
@@ -439,6 +448,27 @@ bool fill_decomp(Decomp &d, const std::vector<Dim> &outer_to_inner) {
     d.ds[k] = 0;
   }
   return true;
+}
+
+// Diagonal walk (Decomp::skew) for a decomposition whose fastest dim steps
+// the source by a large power-of-two-like stride: the dim with the smallest
+// source stride is advanced together with the fastest one, so consecutive
+// work items (lanes, blocks) read -- and write -- at different low address
+// bits instead of all hitting the same L2 sets / channels.  Applied when the
+// fastest dim's source step is >= min_bytes and another dim steps less.
+void set_skew(Decomp &d, const std::vector<Dim> &outer_to_inner, int es, int64_t min_bytes) {
+  d.skew = 0;
+  const int n = (int)outer_to_inner.size();
+  if (n < 2 || min_bytes <= 0) return;
+  const Dim &f = outer_to_inner[n - 1];
+  if (f.n < 2 || std::llabs(f.ss) * es < min_bytes) return;
+  int best = -1;
+  for (int k = 0; k < n - 1; ++k) {
+    const Dim &x = outer_to_inner[k];
+    if (x.n < 2 || std::llabs(x.ss) >= std::llabs(f.ss)) continue;
+    if (best < 0 || std::llabs(x.ss) < std::llabs(outer_to_inner[best].ss)) best = k;
+  }
+  if (best >= 0) d.skew = (n - 1 - best) + 1;  // innermost-first index + 1
 }
 
 int grid_for(uint64_t work_items, uint64_t per_block, uint64_t cap = 256ull * 16) {
@@ -477,6 +507,7 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)outer.size());
     return BM_E_ARG;
   }
+  if (row_bytes <= BM_RC_SKEW_MAXB) set_skew(d, outer, es, BM_RC_SKEW);
   uint64_t rows = 1;
   for (const Dim &x : outer) rows *= (uint64_t)x.n;
   const uint64_t vpr = (uint64_t)(row_bytes / VB);
@@ -636,6 +667,7 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
     return BM_E_ARG;
   }
+  set_skew(td.batch, batch, es, BM_TR_SKEW);
   const Tile tl = pick_tile(td.La, td.Lb, es);
   const int TA = tl.ta, TB = tl.tb;
   const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);

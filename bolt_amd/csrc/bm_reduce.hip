@@ -46,6 +46,9 @@ constexpr int kColsUnroll = BM_COLS_UNROLL;
 #define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
 #endif
 constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
+#ifndef BM_RED_XCD
+#define BM_RED_XCD 0  // rows kernel: blocks dealt to one XCD take consecutive rows (A/B knob)
+#endif
 
 enum Mode {
   M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4, M_MAX = 5, M_MIN = 6,
@@ -591,7 +594,15 @@ template <typename T, int VEC, int MODE>
 __global__ void __launch_bounds__(kThreads)
     k_red_rows(const T *__restrict__ src, RowsDesc d, Sink sk) {
   const int lane = threadIdx.x & 63;
-  const int64_t item = d.item0 + (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  uint64_t bid = blockIdx.x;
+  if (BM_RED_XCD) {
+    // round-robin dispatch puts block b on XCD b % 8: give XCD x the x-th
+    // contiguous eighth of the rows, so the 128-B lines two neighbouring
+    // rows share are fetched into one L2 instead of two
+    const uint64_t g8 = gridDim.x / 8 * 8;
+    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
+  }
+  const int64_t item = d.item0 + (int64_t)bid * (kThreads / 64) + (threadIdx.x >> 6);
   if (item >= d.nitems) return;  // whole wave exits; no block barrier below
   const uint64_t o = fd_div((uint64_t)item, d.nchunks);
   const int64_t c = item - (int64_t)o * (int64_t)d.nchunks.d;
