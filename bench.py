@@ -40,6 +40,9 @@ XGMI_LINK_GBPS = 153.0      # per link, per direction
 
 CONFIGS = {
     # name: (per-GPU shape, dtype, split, description)
+    "C1": ((100, 64, 64), np.float64, 1,
+           "C1: float64 (100,64,64), key 0; swap((0,),(0,)) then sum/mean/var/std at axis=None and "
+           "axis=(0,) of the swapped array (the reference's CPU-runnable case)"),
     "C2": ((2000, 512, 512), np.float32, 1,
            "C2: float32 (2000,512,512) per GPU, key=time; swap((0,),(0,1)) + mean/std over time"),
     "C3": ((4096, 256, 256, 32), np.float32, 2,
@@ -71,7 +74,7 @@ def parse():
     return ap.parse_args()
 
 
-ROOFLINE_KERNEL = {"C2": "k_transpose", "C5": "k_transpose", "C3": "k_rowcopy", "C4": "k_rowcopy",
+ROOFLINE_KERNEL = {"C1": "k_rowcopy", "C2": "k_transpose", "C5": "k_transpose", "C3": "k_rowcopy", "C4": "k_rowcopy",
                    "target64": "k_rowcopy"}
 
 
@@ -150,6 +153,16 @@ def steps_of(cfg, b, world=1):
         return [("swap", lambda: sw.__setitem__("s", b.swap((0,), (0, 1))), 2 * N),
                 ("mean", lambda: sw["s"].mean(axis=2), N + out),
                 ("std", lambda: sw["s"].std(axis=2), N + out)]
+    if cfg == "C1":
+        sw = {}
+        ops = [("swap", lambda: sw.__setitem__("s", b.swap((0,), (0,))), 2 * N)]
+        for name in ("sum", "mean", "var", "std"):
+            for ax in (None, (0,)):
+                nout = 1 if ax is None else n * world // b.shape[1]
+                k = 2 if name in ("var", "std") else 1
+                ops.append(("%s_%s" % (name, "all" if ax is None else "0"),
+                            (lambda name=name, ax=ax: getattr(sw["s"], name)(axis=ax)), N + nout * s * k))
+        return ops
     if cfg == "target64":
         out = (n * world // b.shape[0]) * s
         return [("swap", lambda: b.swap((0,), (0,)), 2 * N),
@@ -226,9 +239,54 @@ def local_numpy_baseline(cfg, shape, dtype):
             "host_cpus": os.cpu_count()}
 
 
+def c1_cpu_baseline(shape, dtype):
+    """C1 in full on one host core: the oracle's record-level restatement of
+    the reference Spark path (8 partitions) and the reference local mode's
+    numpy calls, each repeated to ~10 s."""
+    from oracle import bolt_oracle as O
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(shape).astype(dtype)
+    N = x.nbytes
+    total = 2 * N + 8 * N  # swap + 8 statistics reading the array (outputs are < 33 KB)
+
+    def spark():
+        rs = O.parallelize(x, axis=(0,), npartitions=8)
+        s = O.swap(rs, (0,), (0,))
+        O.sum_(s, None)
+        O.sum_(s, (0,))
+        for name in ("mean", "variance", "stdev"):
+            O.stat(s, name, None)
+            O.stat(s, name, (0,))
+
+    def local():
+        y = np.ascontiguousarray(x.transpose(1, 0, 2))
+        for f in (y.sum, y.mean, y.var, y.std):
+            f()
+            f(axis=0)
+
+    out = {}
+    for name, f in (("spark", spark), ("local", local)):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            f()
+            reps += 1
+            if time.perf_counter() - t0 > (10.0 if name == "spark" else 3.0):
+                break
+        out[name] = (total * reps / (time.perf_counter() - t0) / 1e9, reps)
+    return {"value": out["spark"][0], "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on the whole C1 input, "
+                      "swap + sum/mean/var/std at axis=None and axis=(0,), %d repetitions" % out["spark"][1],
+            "host_cpus": os.cpu_count(),
+            "local_numpy": {"value": round(out["local"][0], 3), "unit": "GB/s", "cores": 1,
+                            "sample": "the reference local mode's numpy calls on the same input, %d repetitions"
+                                      % out["local"][1]}}
+
+
 def cpu_baseline(cfg, shape, dtype, rows):
     """Oracle (record-level restatement of the reference Spark path), 1 core, bounded sample."""
     from oracle import bolt_oracle as O
+    if cfg == "C1":
+        return c1_cpu_baseline(shape, dtype)
     if cfg != "C2":
         return local_numpy_baseline(cfg, shape, dtype)
     rng = np.random.default_rng(0)

@@ -75,6 +75,9 @@ constexpr int kThreads = 256;
 #ifndef BM_TR_SKEW
 #define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
 #endif
+#ifndef BM_TR_PAGEORDER
+#define BM_TR_PAGEORDER 0  // transpose: batch dims ordered by max(|src stride|, |dst stride|), smallest fastest (A/B knob)
+#endif
 #ifndef BM_FUSE
 #define BM_FUSE 1  // fuse short contiguous transpose axes with their continuation (A/B knob)
 #endif
@@ -562,7 +565,14 @@ struct Tile { int ta, tb; };
 constexpr Tile kTiles1[] = {{128, 256}, {128, 128}, {64, 64}, {256, 64}, {64, 256}};
 constexpr Tile kTiles2[] = {{128, 256}, {64, 256}, {64, 64}, {128, 64}, {256, 32}, {32, 256}};
 constexpr Tile kTiles4[] = {{64, 256}, {32, 256}, {64, 64}, {64, 128}, {128, 32}, {256, 16}, {16, 256}, {32, 64}};
+#ifndef BM_T8_SQUARE
+#define BM_T8_SQUARE 0  // f64: 64x64 tiles ahead of 32x64 on equal cost (512-B source segments; A/B knob)
+#endif
+#if BM_T8_SQUARE
+constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {64, 64}, {32, 64}, {64, 32}, {128, 16}, {16, 128}};
+#else
 constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {32, 64}, {64, 64}, {64, 32}, {128, 16}, {16, 128}};
+#endif
 
 template <typename T>
 int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool va_vec, bool vb_vec,
@@ -662,6 +672,15 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
         fused = true;
       }
     }
+  }
+  if (BM_TR_PAGEORDER) {
+    // consecutive tiles step the batch dim with the smallest larger-of-the-two
+    // strides, so they stay inside the same source AND destination pages
+    // (C5 .T: i2, 32 KiB on both sides, instead of i1: 2 MiB in the source;
+    // the UTCL1 misses of profiles/r02_kernel_counters.md)
+    std::stable_sort(batch.begin(), batch.end(), [](const Dim &x, const Dim &y) {
+      return std::max(std::llabs(x.ss), std::llabs(x.ds)) > std::max(std::llabs(y.ss), std::llabs(y.ds));
+    });
   }
   if (!fill_decomp(td.batch, batch)) {
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());

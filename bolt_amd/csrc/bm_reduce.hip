@@ -47,7 +47,7 @@ constexpr int kColsUnroll = BM_COLS_UNROLL;
 #endif
 constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
 #ifndef BM_RED_XCD
-#define BM_RED_XCD 0  // rows kernel: blocks dealt to one XCD take consecutive rows (A/B knob)
+#define BM_RED_XCD 1  // rows kernel: blocks dealt to one XCD take consecutive rows (C2 mean / std +3-4%, profiles/r02_ab_redxcd.log)
 #endif
 
 enum Mode {

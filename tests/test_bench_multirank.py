@@ -17,6 +17,7 @@ ROOT = os.path.dirname(HERE)
 
 # per-rank shard shapes (leading axis grows with the world, as in bench.py)
 SHARDS = {
+    "C1": ((3, 4, 5), np.float64, 1),
     "C2": ((3, 4, 5), np.float32, 1),
     "C3": ((2, 3, 4, 8), np.float32, 2),
     "C4": ((3, 6, 8), np.uint16, 1),
@@ -59,7 +60,12 @@ def _body(rank, world):
         results = {name: call() for name, call, _ in ops}
         assert all(nb > 0 for _, _, nb in ops)
         x = full.astype(np.float64)
-        if cfg == "C2":
+        if cfg == "C1":
+            y = x.transpose(1, 0, 2)
+            for name in ("sum", "mean", "var", "std"):
+                assert np.allclose(results[name + "_all"], getattr(y, name)(), rtol=1e-12), name
+                assert np.allclose(results[name + "_0"], getattr(y, name)(axis=0), rtol=1e-12), name
+        elif cfg == "C2":
             s = b.swap((0,), (0, 1))
             assert np.asarray(s.toarray()).tobytes() == np.ascontiguousarray(full.transpose(1, 2, 0)).tobytes()
             assert np.allclose(results["mean"], x.mean(0), rtol=1e-6)

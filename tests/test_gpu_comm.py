@@ -97,3 +97,49 @@ def test_exchange_helpers_with_a_comm(comm):
     recv, work = D.all_to_all_bytes(ctx, x, [x.numel()], [x.numel()], 8, async_op=True)
     work.wait()
     assert torch.equal(recv, x)
+
+
+_CHILD = r"""
+import os, sys
+sys.path.insert(0, os.environ["BM_ROOT"])
+import numpy as np, torch, torch.distributed as dist
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ["BM_PORT"])
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+from bolt_amd import MI355XContext
+from bolt_amd.mi355x import dist as D
+ctx = MI355XContext(device="cuda:0")
+assert ctx.comm is None          # world 1: no exchange, no communicator
+ctx._init_comm()                 # the rendezvous-store path an N-GPU context takes
+assert ctx.comm is not None and ctx.comm_stream is not None
+x = torch.arange(1 << 20, dtype=torch.int32, device="cuda").view(torch.uint8)
+recv, work = D._rccl_all_to_all(ctx, x, [x.numel()], [x.numel()], async_op=True)
+work.wait()
+assert torch.equal(recv, x)
+g = D._rccl_all_gather(ctx, x[:4096], [4096])
+assert torch.equal(g, x[:4096])
+ctx.close()
+assert ctx.comm is None
+dist.destroy_process_group()
+print("child ok")
+"""
+
+
+def test_context_opens_its_communicator_through_the_store():
+    """MI355XContext._init_comm on a one-rank nccl group, in a child process:
+    rank 0 makes the id, publishes it in the rendezvous store, bm_comm_init,
+    an exchange on the context's RCCL stream, close()."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, BM_ROOT=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), BM_PORT=str(port))
+    r = subprocess.run([sys.executable, "-c", _CHILD], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

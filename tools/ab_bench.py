@@ -99,7 +99,7 @@ class RecGather(object):
     """C5's chunk pack ((16,16), padding 2 on 64x64 float64 records) or its
     values_to_keys((0,)) repack, as one bm_record_gather (parts as _ops picks)."""
 
-    def __init__(self, kind, nparts_off=False):
+    def __init__(self, kind, nparts_off=False, part_bytes=None):
         import os
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from bolt_amd.mi355x import plan, _ops
@@ -113,7 +113,7 @@ class RecGather(object):
             rmap = plan.copies_to_map(plan.v2k_copies(geom, new, [], vmask), 64 * new.size)
             self.src_rec = geom.size
         self.dst_rec = rmap.size
-        parts = [] if nparts_off else _ops.record_parts(rmap, self.src_rec, 8)
+        parts = [] if nparts_off else _ops.record_parts(rmap, self.src_rec, 8, part_bytes)
         self.nparts, self.parts = len(parts) // 4, (i64(parts) if parts else None)
         self.map = torch.from_numpy(rmap).cuda()
         self.src = torch.randint(0, 255, (self.nrec * self.src_rec * 8,), dtype=torch.uint8, device="cuda")
@@ -156,6 +156,8 @@ OPS = {
     "c5_pack_whole": lambda: RecGather("pack", True),
     "c5_v2k": lambda: RecGather("v2k"),
     "c5_v2k_whole": lambda: RecGather("v2k", True),
+    "c5_v2k_pb16k": lambda: RecGather("v2k", part_bytes=16 << 10),
+    "c5_v2k_pb24k": lambda: RecGather("v2k", part_bytes=24 << 10),
     "c2_copy": lambda: Copy(2097152000),
     "c2_swap": lambda: Permute((2000, 512 * 512), (1, 0), np.float32),
     "c2_mean_rows": lambda: Reduce(0, 512 * 512, 2000, 1, np.float32, np.float32),
