@@ -46,6 +46,9 @@ constexpr int kColsUnroll = BM_COLS_UNROLL;
 #define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
 #endif
 constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
+#ifndef BM_INT_UNROLL
+#define BM_INT_UNROLL 8  // exact-integer column var: rows in flight per lane (C4 var 3.76 -> 3.47 ms over 4, profiles/r02_ab_int.log)
+#endif
 #ifndef BM_RED_XCD
 #define BM_RED_XCD 1  // rows kernel: blocks dealt to one XCD take consecutive rows (C2 mean / std +3-4%, profiles/r02_ab_redxcd.log)
 #endif
@@ -377,9 +380,13 @@ struct ColsDesc {
 template <typename T, int VEC, int MODE>
 __global__ void __launch_bounds__(kThreads)
     k_red_cols(const T *__restrict__ src, ColsDesc d, Sink sk) {
-  __shared__ double sm0[kThreads * VEC];
-  __shared__ double sm1[(MODE == M_MOM) ? kThreads * VEC : 1];
-  __shared__ double smn[(MODE == M_MOM) ? kThreads : 1];
+  // row-phase merge buffers, dynamic: sized only when the block has more
+  // than one row phase (cols_lds_bytes), so the wide-output case (C4's var,
+  // one phase) keeps the occupancy of an LDS-free kernel
+  extern __shared__ double smem[];
+  double *sm0 = smem;
+  double *sm1 = smem + kThreads * VEC;
+  double *smn = smem + 2 * kThreads * VEC;
   const uint64_t ot = (uint64_t)d.tile0 + blockIdx.x;
   const uint64_t o = fd_div(ot, d.ntc);
   const uint64_t tc = ot - o * d.ntc.d;
@@ -734,6 +741,183 @@ __global__ void __launch_bounds__(kThreads)
   emit<MODE>(sk, idx, ntot, m, 0.0, us);
 }
 
+// ----------------------------------------------- exact integer var / std --
+// 1- and 2-byte integer (and bool) inputs: var / std from exact integer sums.
+// Each lane keeps S1 = sum x (int64) and S2 = sum x^2 (uint64; x^2 < 2^32);
+// lanes, row phases and waves add exactly (any order gives the same bits),
+// and M2 = (n S2 - S1^2) / n is formed in 128-bit integers and rounded once
+// -- exact up to that rounding, cheaper than the float64 Welford path (no
+// conversions, one multiply-add per element) and deterministic by
+// construction.  (statcounter.py:51-59 computes the same M2 in float64.)
+template <typename T> constexpr bool small_int() {
+  return std::is_integral<T>::value && sizeof(T) <= 2;
+}
+
+// x^2 of a value of a 1- or 2-byte type, in 32-bit unsigned arithmetic (< 2^32)
+__device__ __forceinline__ uint64_t sq32(int32_t x) {
+  const uint32_t a = (uint32_t)(x < 0 ? -x : x);
+  return (uint64_t)(a * a);
+}
+
+// (n, S1, S2) -> (mean, M2) with the n S2 - S1^2 difference in 128 bits
+__device__ __forceinline__ void int_moments(uint64_t n, int64_t s1, uint64_t s2, double &mean, double &m2) {
+  mean = n ? (double)s1 / (double)n : 0.0;
+  const uint64_t a1 = (uint64_t)(s1 < 0 ? -s1 : s1);
+  // n * s2 and a1 * a1 as (hi, lo)
+  const uint64_t p_lo = n * s2, p_hi = __umul64hi(n, s2);
+  const uint64_t q_lo = a1 * a1, q_hi = __umul64hi(a1, a1);
+  const uint64_t lo = p_lo - q_lo;
+  const uint64_t hi = p_hi - q_hi - (p_lo < q_lo ? 1 : 0);
+  const double num = (double)hi * 18446744073709551616.0 + (double)lo;  // >= 0 (Cauchy-Schwarz)
+  m2 = n ? num / (double)n : 0.0;
+}
+
+// chunk partials (workspace) stay exact integer sums, merged by the combine
+// kernel's integer branch; final outputs and rank states get (mean, M2)
+__device__ __forceinline__ void emit_int_mom(const Sink &sk, int64_t idx, int64_t e, int64_t c, int64_t n,
+                                             int64_t s1, uint64_t s2) {
+  if (!sk.final_out && sk.shifted) {
+    reinterpret_cast<int64_t *>(sk.p0)[idx] = s1;
+    reinterpret_cast<uint64_t *>(sk.p1)[idx] = s2;
+    return;
+  }
+  double mean, m2;
+  int_moments((uint64_t)n, s1, s2, mean, m2);
+  emit_mom(sk, idx, e, c, (double)n, mean, m2, 0.0);
+}
+
+template <typename T, int VEC>
+__global__ void __launch_bounds__(kThreads)
+    k_red_cols_int(const T *__restrict__ src, ColsDesc d, Sink sk) {
+  extern __shared__ double smem[];
+  uint64_t *l1 = reinterpret_cast<uint64_t *>(smem);
+  uint64_t *l2 = l1 + kThreads * VEC;
+  const uint64_t ot = (uint64_t)d.tile0 + blockIdx.x;
+  const uint64_t o = fd_div(ot, d.ntc);
+  const uint64_t tc = ot - o * d.ntc.d;
+  const int64_t c = blockIdx.y;
+  const int64_t r_lo = c * d.rchunk;
+  const int64_t r_hi = min(d.R, r_lo + d.rchunk);
+  const int cv = threadIdx.x % d.tcv;
+  const int ph = threadIdx.x / d.tcv;
+  const int64_t col0 = ((int64_t)tc * d.tcv + cv) * VEC;
+  const bool active = col0 < d.I;
+  const int64_t nph = d.nph;
+  int64_t s1[VEC];
+  uint64_t s2[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) { s1[k] = 0; s2[k] = 0; }
+  if (active) {
+    const T *base = src + ((int64_t)o * d.R) * d.I + col0;
+    int64_t r = r_lo + ph;
+    constexpr int U = BM_INT_UNROLL;  // rows in flight per lane
+    for (; r + (U - 1) * nph < r_hi; r += U * nph) {
+      T v[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) vload_nt<T, VEC>(base + (r + u * nph) * d.I, v[u]);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        int32_t t1 = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int32_t x = (int32_t)v[u][k];
+          t1 += x;
+          s2[k] += sq32(x);
+        }
+        s1[k] += t1;
+      }
+    }
+    for (; r < r_hi; r += nph) {
+      T v[VEC];
+      vload_nt<T, VEC>(base + r * d.I, v);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const int32_t x = (int32_t)v[k];
+        s1[k] += x;
+        s2[k] += sq32(x);
+      }
+    }
+  }
+  if (nph > 1) {  // row phases: exact integer sums
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      l1[threadIdx.x * VEC + k] = (uint64_t)s1[k];
+      l2[threadIdx.x * VEC + k] = s2[k];
+    }
+    __syncthreads();
+    if (ph == 0) {
+      for (int p = 1; p < nph; ++p) {
+        const int other = p * d.tcv + cv;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          s1[k] += (int64_t)l1[other * VEC + k];
+          s2[k] += l2[other * VEC + k];
+        }
+      }
+    }
+  }
+  if (ph != 0 || !active) return;
+  const int64_t n = r_hi - r_lo;
+  const int64_t plane = d.O * d.I;
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) {
+    const int64_t e = (int64_t)o * d.I + col0 + k;
+    const int64_t idx = sk.final_out ? e : (c * plane + e);
+    emit_int_mom(sk, idx, e, c, n, s1[k], s2[k]);
+  }
+}
+
+template <typename T, int VEC>
+__global__ void __launch_bounds__(kThreads)
+    k_red_rows_int(const T *__restrict__ src, RowsDesc d, Sink sk) {
+  const int lane = threadIdx.x & 63;
+  uint64_t bid = blockIdx.x;
+  if (BM_RED_XCD) {
+    const uint64_t g8 = gridDim.x / 8 * 8;
+    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
+  }
+  const int64_t item = d.item0 + (int64_t)bid * (kThreads / 64) + (threadIdx.x >> 6);
+  if (item >= d.nitems) return;  // whole wave exits
+  const uint64_t o = fd_div((uint64_t)item, d.nchunks);
+  const int64_t c = item - (int64_t)o * (int64_t)d.nchunks.d;
+  const int64_t r_lo = c * d.rchunk;
+  const int64_t r_hi = min(d.R, r_lo + d.rchunk);
+  const T *row = src + (int64_t)o * d.R;
+  int64_t s1 = 0;
+  uint64_t s2 = 0;
+  const int64_t stride = 64 * VEC;
+  for (int64_t j = r_lo + (int64_t)lane * VEC; j < r_hi; j += stride) {
+    if (j + VEC <= r_hi) {
+      T v[VEC];
+      vload_nt<T, VEC>(row + j, v);
+      int32_t t1 = 0;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const int32_t x = (int32_t)v[k];
+        t1 += x;
+        s2 += sq32(x);
+      }
+      s1 += t1;
+    } else {
+      for (int64_t k = j; k < r_hi; ++k) {
+        const int32_t x = (int32_t)row[k];
+        s1 += x;
+        s2 += sq32(x);
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    s1 += (int64_t)__shfl_xor((long long)s1, off);
+    s2 += (uint64_t)__shfl_xor((long long)s2, off);
+  }
+  if (lane != 0) return;
+  const int64_t n = r_hi - r_lo;
+  const int64_t e = (int64_t)o;
+  const int64_t idx = sk.final_out ? e : (c * d.O + e);
+  emit_int_mom(sk, idx, e, c, n, s1, s2);
+}
+
 // --------------------------------------------------------------- combine --
 constexpr int kMaxParts = 256;  // parts per bm_reduce_combine (ranks of a merge); kernarg-resident counts
 struct CombDesc {
@@ -743,6 +927,8 @@ struct CombDesc {
   int64_t R, rchunk;    // uniform chunk counts when explicit == 0
   int32_t explicit_counts;
   int32_t pivots;       // var / std chunk partials: p0 is mean - P, P in the plane after M2
+  int32_t int_sums;     // var / std of 1-2 byte integers: partials are exact (S1, S2) sums
+  int32_t pad_;
   int64_t counts[kMaxParts];
 };
 
@@ -754,6 +940,24 @@ __global__ void __launch_bounds__(kThreads)
     double n = 0.0, m = 0.0, q = 0.0;
     uint64_t u = 0;
     bool first = true;
+    if constexpr (MODE == M_MOM) {
+      if (d.int_sums) {  // exact: add the chunks' integer sums
+        int64_t s1 = 0, cnt = 0;
+        uint64_t s2 = 0;
+        for (int64_t p = 0; p < d.nparts; ++p) {
+          const int64_t nb = min(d.R, (p + 1) * d.rchunk) - p * d.rchunk;
+          if (nb <= 0) continue;
+          const int64_t at = p * d.part_stride + e;
+          s1 += reinterpret_cast<const int64_t *>(p0)[at];
+          s2 += reinterpret_cast<const uint64_t *>(p1)[at];
+          cnt += nb;
+        }
+        double mean, m2;
+        int_moments((uint64_t)cnt, s1, s2, mean, m2);
+        emit_mom(sk, e, e, 1, (double)cnt, mean, m2, 0.0);
+        continue;
+      }
+    }
     for (int64_t p = 0; p < d.nparts; ++p) {
       const double nb = d.explicit_counts
                             ? (double)d.counts[p]
@@ -881,10 +1085,62 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
   return p;
 }
 
+// exact integer var / std: the same grids as the float kernels
+template <typename T>
+int launch_int_mom(const RedPlan &p, const T *s, int64_t O, int64_t R, int64_t I, Sink sk, hipStream_t st) {
+  if (p.rows) {
+    RowsDesc d;
+    d.O = O; d.R = R; d.rchunk = p.rchunk;
+    d.nchunks = make_fastdiv((uint64_t)p.nchunks);
+    d.nitems = O * p.nchunks;
+    const int64_t blocks = cdiv(d.nitems, kThreads / 64);
+    for (int64_t b0 = 0; b0 < blocks; b0 += kMaxBlocks) {
+      const int g = (int)std::min<int64_t>(kMaxBlocks, blocks - b0);
+      d.item0 = b0 * (kThreads / 64);
+      switch (p.vec) {
+        case 16: if constexpr (sizeof(T) == 1) { k_red_rows_int<T, 16><<<g, kThreads, 0, st>>>(s, d, sk); } break;
+        case 8: k_red_rows_int<T, 8><<<g, kThreads, 0, st>>>(s, d, sk); break;
+        case 4: k_red_rows_int<T, 4><<<g, kThreads, 0, st>>>(s, d, sk); break;
+        case 2: k_red_rows_int<T, 2><<<g, kThreads, 0, st>>>(s, d, sk); break;
+        default: k_red_rows_int<T, 1><<<g, kThreads, 0, st>>>(s, d, sk); break;
+      }
+    }
+    return BM_OK;
+  }
+  ColsDesc d;
+  d.O = O; d.R = R; d.I = I;
+  d.rchunk = p.rchunk; d.nchunks = p.nchunks;
+  d.tcv = p.tcv; d.nph = p.nph;
+  d.ntc = make_fastdiv((uint64_t)p.ntc);
+  const int64_t bx = O * p.ntc;
+  const int64_t per = std::max<int64_t>(1, kMaxBlocks / p.nchunks);
+  for (int64_t t0 = 0; t0 < bx; t0 += per) {
+    d.tile0 = t0;
+    dim3 grid((unsigned)std::min<int64_t>(per, bx - t0), (unsigned)p.nchunks);
+    const size_t lds = p.nph > 1 ? 2 * (size_t)kThreads * p.vec * sizeof(uint64_t) : 0;
+    switch (p.vec) {
+      case 8: k_red_cols_int<T, 8><<<grid, kThreads, lds, st>>>(s, d, sk); break;
+      case 4: k_red_cols_int<T, 4><<<grid, kThreads, lds, st>>>(s, d, sk); break;
+      case 2: k_red_cols_int<T, 2><<<grid, kThreads, lds, st>>>(s, d, sk); break;
+      default: k_red_cols_int<T, 1><<<grid, kThreads, lds, st>>>(s, d, sk); break;
+    }
+  }
+  return BM_OK;
+}
+
+// dynamic LDS of a k_red_cols launch: the row-phase buffers when nph > 1
+template <int MODE> size_t cols_lds_bytes(int nph, int vec) {
+  if (nph <= 1) return 0;
+  return (MODE == M_MOM ? (2 * (size_t)kThreads * vec + kThreads) : (size_t)kThreads * vec) * sizeof(double);
+}
+
 template <typename T, int MODE>
 int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64_t I, Sink sk,
                   hipStream_t st) {
   const T *s = (const T *)src;
+  if constexpr (MODE == M_MOM && small_int<T>()) {
+    return launch_int_mom<T>(p, s, O, R, I, sk, st);
+  }
   if (p.rows) {
     RowsDesc d;
     d.O = O; d.R = R; d.rchunk = p.rchunk;
@@ -916,9 +1172,9 @@ int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64
       dim3 grid((unsigned)std::min<int64_t>(per, bx - t0), (unsigned)p.nchunks);
       switch (p.vec) {
 #define BM_COLS_CASE(V) \
-  case V: if constexpr (V * sizeof(T) <= 16) { k_red_cols<T, V, MODE><<<grid, kThreads, 0, st>>>(s, d, sk); } break;
+  case V: if constexpr (V * sizeof(T) <= 16) { k_red_cols<T, V, MODE><<<grid, kThreads, cols_lds_bytes<MODE>(p.nph, V), st>>>(s, d, sk); } break;
         BM_COLS_CASE(8) BM_COLS_CASE(4) BM_COLS_CASE(2)
-        default: k_red_cols<T, 1, MODE><<<grid, kThreads, 0, st>>>(s, d, sk); break;
+        default: k_red_cols<T, 1, MODE><<<grid, kThreads, cols_lds_bytes<MODE>(p.nph, 1), st>>>(s, d, sk); break;
 #undef BM_COLS_CASE
       }
     }
@@ -1079,7 +1335,8 @@ int run_reduce(int stat, const void *src, int dt, int64_t O, int64_t R, int64_t 
   cd.R = R;
   cd.rchunk = p.rchunk;
   cd.explicit_counts = 0;
-  cd.pivots = mode == M_MOM;
+  cd.int_sums = mode == M_MOM && !is_float(dt) && dtype_size(dt) <= 2;
+  cd.pivots = mode == M_MOM && !cd.int_sums;
   rc = launch_combine(mode, dt, w0, w1, cd, sk, st);
   if (rc) return rc;
   return check_launch(who);

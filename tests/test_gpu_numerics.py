@@ -95,3 +95,28 @@ def test_float32_offset(gpu_ctx):
     t = x.astype(np.longdouble).var(axis=1)
     err = np.abs(v.astype(np.longdouble) - t) / t
     assert float(err.max()) <= 1e-6
+
+
+@pytest.mark.parametrize("dtype", [np.uint16, np.int16, np.uint8, np.int8, np.bool_])
+@pytest.mark.parametrize("axis", [0, 1])
+def test_small_int_var_is_exact(gpu_ctx, dtype, axis):
+    """1- and 2-byte integer var / std come from exact integer sums: every
+    output within 2 ulp of the exact rational variance (Python integers)."""
+    rng = np.random.default_rng(11)
+    shape = (3000, 257)
+    if dtype == np.bool_:
+        x = rng.integers(0, 2, size=shape).astype(bool)
+    else:
+        info = np.iinfo(dtype)
+        x = rng.integers(info.max - 40, info.max, size=shape, endpoint=True).astype(dtype)
+        x[::7] = info.min  # extreme spread
+    b = bolt.array(x, gpu_ctx, axis=(0,))
+    v = np.asarray(b.var(axis=axis))
+    xi = x.astype(np.int64)
+    n = x.shape[axis]
+    s1 = xi.sum(axis=axis)
+    s2 = (xi * xi).sum(axis=axis)
+    for k in range(0, v.size, 17):
+        num = int(n) * int(s2.reshape(-1)[k]) - int(s1.reshape(-1)[k]) ** 2
+        exact = num / (n * n)   # Python int / int: correctly rounded
+        assert abs(v.reshape(-1)[k] - exact) <= 2 * np.spacing(exact) + 1e-300, (k, v.reshape(-1)[k], exact)

@@ -72,7 +72,7 @@ class Reduce(object):
         self.src = (torch.randn(n // 4, device="cuda") * 50 + 1000).view(torch.uint8) \
             if np.dtype(dtype) == np.float32 else torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")
         self.out = torch.empty(O * I * np.dtype(out_dtype).itemsize, dtype=torch.uint8, device="cuda")
-        self.ws = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
+        self.ws = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
         self.bytes = n + self.out.numel()
 
     def __call__(self, lib):
@@ -179,6 +179,8 @@ OPS = {
     "t64_mean_cols": lambda: Reduce(0, 1, 4096, 2097152, np.float32, np.float32),
     "t64_std_cols": lambda: Reduce(2, 1, 4096, 2097152, np.float32, np.float32),
     "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
+    "c4_var_full": lambda: Reduce(1, 1, 10000, 1024 * 1024, np.uint16, np.float64),
+    "u16_var_rows": lambda: Reduce(1, 1024 * 1024, 2000, 1, np.uint16, np.float64),
     "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),
     "c5_perm": lambda: Permute((64, 64, 64, 64, 64), (2, 0, 4, 1, 3), np.float64),
 }

@@ -14,6 +14,8 @@
 //           fastest.  T = 16, 32, 64.
 //   diagTg  the same with runs of g rows contiguous along c (g = 4: 512-B
 //           destination runs, 4 source lines per h)
+//   ldsT    T x T record tiles transposed through LDS: T*128-B contiguous
+//           runs on both the source and the destination side
 // Build: hipcc -O3 --offload-arch=gfx950 -o /tmp/rcs.bin tools/skew/rowcopy_skew.hip
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -75,6 +77,45 @@ __global__ void __launch_bounds__(256) k_diag(const u4* __restrict__ src, u4* __
   for (int u = 0; u < U; ++u) __builtin_nontemporal_store(r[u], dst + dof[u]);
 }
 
+
+// Record-tile transpose through LDS: a T x T tile of 128-B records (T h by
+// T c) is read as T source runs of T*128 B (one c each) and written as T
+// destination runs of T*128 B (one h each): long contiguous runs on BOTH
+// sides, the records re-ordered in LDS (row pitch padded by one 16-B vector).
+template <int T>
+__global__ void __launch_bounds__(256) k_ldsT(const u4* __restrict__ src, u4* __restrict__ dst) {
+  constexpr uint64_t H = A * B;
+  constexpr int RV = T * 8;                 // 16-B vectors per tile row (T records)
+  constexpr int NV = T * RV;                // vectors per tile
+  constexpr int PER = NV / 256;             // vectors per thread
+  __shared__ u4 tile[T][RV + 1];
+  const uint64_t ntc = C / T;
+  for (uint64_t t = blockIdx.x; t < (H / T) * ntc; t += gridDim.x) {
+    const uint64_t c0 = (t % ntc) * T, h0 = (t / ntc) * T;
+    u4 r[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      const int cl = q / RV, w = q % RV;    // tile row = one c; w = h_local * 8 + v
+      r[i] = __builtin_nontemporal_load(src + ((c0 + cl) * H + h0) * 8 + w);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      tile[q / RV][q % RV] = r[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      const int hl = q / RV, w = q % RV;    // output row = one h; w = c_local * 8 + v
+      const int cl = w / 8, v = w % 8;
+      __builtin_nontemporal_store(tile[cl][hl * 8 + v], dst + ((h0 + hl) * C + c0) * 8 + w);
+    }
+    __syncthreads();
+  }
+}
+
 static bool check(const u4* dsrc, const u4* ddst) {
   for (int t = 0; t < 64; ++t) {
     const uint64_t c = (t * 977) % C, a = (t * 131) % A, b = (t * 37 + 5) % B;
@@ -127,6 +168,8 @@ int main() {
     run("diag32g4", [&] { k_diag<U, 32, 4><<<g4, 256>>>(src, dst); }, src, dst);
     run("diag64g4", [&] { k_diag<U, 64, 4><<<g4, 256>>>(src, dst); }, src, dst);
     run("diag64g8", [&] { k_diag<U, 64, 8><<<g4, 256>>>(src, dst); }, src, dst);
+    run("lds8", [&] { k_ldsT<8><<<262144, 256>>>(src, dst); }, src, dst);
+    run("lds16", [&] { k_ldsT<16><<<262144, 256>>>(src, dst); }, src, dst);
   }
   return 0;
 }
