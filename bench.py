@@ -421,9 +421,13 @@ def main():
         elapsed = time.perf_counter() - t0
         be.permute = permute0
         phases = {}
+        rccl_ms = None
         if bdist.PROFILE is not None:
             for k, evs in bdist.PROFILE.items():
                 phases[k] = float(np.mean([a.elapsed_time(z) for a, z in evs]))
+            if bdist.PROFILE.get("rccl"):
+                # the RCCL groups alone (all pipeline stages of a swap), per swap
+                rccl_ms = float(np.sum([a.elapsed_time(z) for a, z in bdist.PROFILE["rccl"]])) / steps
             bdist.PROFILE = None
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -497,6 +501,12 @@ def main():
                             "peak": peak, "unit": "GB/s per rank (egress)",
                             "frac": round(payload / (a2a / 1e3) / 1e9 / peak, 4) if a2a else None,
                             "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
+            if rccl_ms:
+                # isolated: hipEvents around each bm_alltoallv on the RCCL stream
+                # (stages overlap pack / unpack, so this is the links' own time)
+                line["xgmi"]["rccl_ms_per_swap"] = round(rccl_ms, 4)
+                line["xgmi"]["rccl_achieved"] = round(payload / (rccl_ms / 1e3) / 1e9, 1)
+                line["xgmi"]["rccl_frac"] = round(payload / (rccl_ms / 1e3) / 1e9 / peak, 4)
         line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
         line["roofline"]["measured_copy_peak"] = HBM_COPY_GBPS
         return line

@@ -134,9 +134,15 @@ def _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op):
         recv.record_stream(stream)
     sp = send.data_ptr() if send.numel() else None
     rp = recv.data_ptr() if recv.numel() else None
+    if PROFILE is not None:  # the RCCL group alone, on the stream it runs on
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record(stream)
     _lib.check(_lib.load().bm_alltoallv(ctx.comm, sp, _lib.i64_array(send_sizes), _lib.i64_array(_offsets(send_sizes)),
                                         rp, _lib.i64_array(recv_sizes), _lib.i64_array(_offsets(recv_sizes)),
                                         stream.cuda_stream), "bm_alltoallv")
+    if PROFILE is not None:
+        ev[1].record(stream)
+        PROFILE.setdefault("rccl", []).append(ev)
     if not async_op:
         return recv
     done = torch.cuda.Event()
