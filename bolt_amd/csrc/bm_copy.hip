@@ -72,6 +72,9 @@ constexpr int kThreads = 256;
 #ifndef BM_RC_SKEW_MAXB
 #define BM_RC_SKEW_MAXB 256  // ... and rows are at most this many bytes (longer rows already spread over L2 channels)
 #endif
+#ifndef BM_RC_DIAG
+#define BM_RC_DIAG 0  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this (0 = off; A/B knob)
+#endif
 #ifndef BM_TR_SKEW
 #define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
 #endif
@@ -93,10 +96,33 @@ constexpr uint64_t kMaxGrid = 0xffffffffull / 1024;
 constexpr int kUnroll = BM_RC_UNROLL;
 
 // ---------------------------------------------------------------- rowcopy --
+// 16x16 diagonal tiles over the two fastest row dims (c fastest, g next, in
+// destination order): the 16 rows of a diagonal have distinct g AND distinct c,
+// so neither side of a block's rows shares the low address bits of a large
+// power-of-two stride, while a 16x16 tile keeps both sides' pages local
+// (tools/skew/rowcopy_skew.hip "diag16").  A bijection inside each tile.
+struct Diag16 {
+  int on;
+  int pad_;
+  FastDiv grp;   // Ng * Nc rows per (outer) group
+  FastDiv ntc;   // Nc / 16 tiles along c
+  uint64_t nc;   // Nc
+};
+
+__device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
+  const uint64_t outer = fd_div(row, t.grp);
+  const uint64_t q = row - outer * t.grp.d;
+  const uint64_t tile = q >> 8, w = q & 255;
+  const uint64_t gt = fd_div(tile, t.ntc), ct = tile - gt * t.ntc.d;
+  const uint64_t j = w >> 4, k = w & 15;
+  const uint64_t g = gt * 16 + k, c = ct * 16 + ((k + j) & 15);
+  return outer * t.grp.d + g * t.nc + c;
+}
+
 template <int VB>
 __global__ void __launch_bounds__(kRcThreads)
     k_rowcopy(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
-              FastDiv vpr, uint64_t total, int es, int xcd) {
+              FastDiv vpr, uint64_t total, int es, int xcd, Diag16 dg) {
   typedef typename VecB<VB>::t V;
   const uint64_t step = (uint64_t)gridDim.x * kRcThreads * kUnroll;
   // xcd: the grid covers the copy (a multiple of 8 blocks); blocks dealt to
@@ -115,7 +141,7 @@ __global__ void __launch_bounds__(kRcThreads)
         const uint64_t row = fd_div(g, vpr);
         const uint64_t v = g - row * vpr.d;
         int64_t so, dof;
-        decomp2(row, d, so, dof);
+        decomp2(dg.on ? diag16_row(row, dg) : row, d, so, dof);
         reg[u] = __builtin_nontemporal_load(reinterpret_cast<const V *>(src + so * es + (int64_t)v * VB));
         doff[u] = dof * es + (int64_t)v * VB;
       }
@@ -511,6 +537,22 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     return BM_E_ARG;
   }
   if (row_bytes <= BM_RC_SKEW_MAXB) set_skew(d, outer, es, BM_RC_SKEW);
+  Diag16 dg{};
+  {
+    // 16x16 diagonal tiles when the fastest row dim steps the source by a
+    // large stride and the next one by less (C3 / 64 GiB swaps: c then b)
+    const int n = (int)outer.size();
+    if (BM_RC_DIAG && row_bytes <= BM_RC_SKEW_MAXB && n >= 2 && d.skew == 0) {
+      const Dim &f = outer[n - 1], &g = outer[n - 2];
+      if (f.n % 16 == 0 && g.n % 16 == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
+          std::llabs(g.ss) < std::llabs(f.ss)) {
+        dg.on = 1;
+        dg.grp = make_fastdiv((uint64_t)(f.n * g.n));
+        dg.ntc = make_fastdiv((uint64_t)(f.n / 16));
+        dg.nc = (uint64_t)f.n;
+      }
+    }
+  }
   uint64_t rows = 1;
   for (const Dim &x : outer) rows *= (uint64_t)x.n;
   const uint64_t vpr = (uint64_t)(row_bytes / VB);
@@ -528,11 +570,11 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     grid = grid_for(total, per, BM_RC_GRIDCAP);
   }
   switch (VB) {
-    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
-    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
-    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
-    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
-    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd); break;
+    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
+    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
+    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
+    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
+    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
   }
   return BM_OK;
 }

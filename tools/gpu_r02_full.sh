@@ -3,7 +3,7 @@
 # line, and C3 / C4 / C5 bench lines with their rocprofv3 kernel summaries.
 set -o pipefail
 export TMPDIR=/tmp
-T=${TAG:-r02i}
+T=${TAG:-r02l}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$T.log 2>&1 || { echo TESTS_FAIL; tail -40 gpurun_out/gpu_tests_$T.log; exit 1; }
 tail -2 gpurun_out/gpu_tests_$T.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$T.log 2>&1 || { echo SMOKE_FAIL; tail gpurun_out/smoke_$T.log; exit 1; }
