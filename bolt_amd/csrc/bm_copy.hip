@@ -73,13 +73,16 @@ constexpr int kThreads = 256;
 #define BM_RC_SKEW_MAXB 256  // ... and rows are at most this many bytes (longer rows already spread over L2 channels)
 #endif
 #ifndef BM_RC_DIAG
-#define BM_RC_DIAG 0  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this (0 = off; A/B knob)
+#define BM_RC_DIAG 65536  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this many bytes (0 = off): C3 +8-9%, 64 GiB target +13-15% (profiles/r02_ab_diag.log)
 #endif
 #ifndef BM_TR_SKEW
 #define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
 #endif
 #ifndef BM_TR_PAGEORDER
 #define BM_TR_PAGEORDER 0  // transpose: batch dims ordered by max(|src stride|, |dst stride|), smallest fastest (A/B knob)
+#endif
+#ifndef BM_TR_LOOP
+#define BM_TR_LOOP 0  // transpose: each block walks the batch dim that is page-local on both sides, if >= this many blocks remain (0 = off; A/B knob)
 #endif
 #ifndef BM_FUSE
 #define BM_FUSE 1  // fuse short contiguous transpose axes with their continuation (A/B knob)
@@ -618,8 +621,8 @@ constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {32, 64}, {64, 64}, {64, 32}, 
 
 template <typename T>
 int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool va_vec, bool vb_vec,
-                       bool fused, hipStream_t st) {
-  uint64_t g = td.ntiles;
+                       bool fused, hipStream_t st, uint64_t loop_n = 1) {
+  uint64_t g = td.ntiles / loop_n;
   if (g > kMaxGrid) g = kMaxGrid;  // grid-stride beyond the launch limit
   const int grid = (int)g;
 #define BM_TILE(A, B) \
@@ -724,17 +727,35 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
       return std::max(std::llabs(x.ss), std::llabs(x.ds)) > std::max(std::llabs(y.ss), std::llabs(y.ds));
     });
   }
-  if (!fill_decomp(td.batch, batch)) {
-    bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
-    return BM_E_ARG;
-  }
-  set_skew(td.batch, batch, es, BM_TR_SKEW);
   const Tile tl = pick_tile(td.La, td.Lb, es);
   const int TA = tl.ta, TB = tl.tb;
   const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);
   const uint64_t ntB = (uint64_t)((td.Lb + TB - 1) / TB);
   uint64_t nb = 1;
   for (const Dim &x : batch) nb *= (uint64_t)x.n;
+  // Each block walks the batch dim whose source AND destination strides are
+  // smallest (C5 .T: i2, 32 KiB on both sides): its tiles then stay inside the
+  // same source and destination pages (UTCL1 misses, profiles/
+  // r02_kernel_counters.md).  The dim becomes the slowest of the tile index
+  // and the grid covers the rest, so the grid-stride loop steps it.
+  uint64_t loop_n = 1;
+  if (BM_TR_LOOP && !batch.empty()) {
+    int best = -1;
+    int64_t best_m = 0;
+    for (int k = 0; k < (int)batch.size(); ++k) {
+      const int64_t m = std::max(std::llabs(batch[k].ss), std::llabs(batch[k].ds));
+      if (batch[k].n >= 8 && (best < 0 || m < best_m)) best = k, best_m = m;
+    }
+    if (best >= 0 && best_m * es <= 65536 && ntA * ntB * (nb / (uint64_t)batch[best].n) >= (uint64_t)BM_TR_LOOP) {
+      loop_n = (uint64_t)batch[best].n;
+      std::rotate(batch.begin(), batch.begin() + best, batch.begin() + best + 1);
+    }
+  }
+  if (!fill_decomp(td.batch, batch)) {
+    bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
+    return BM_E_ARG;
+  }
+  set_skew(td.batch, batch, es, BM_TR_SKEW);
   td.ntB = make_fastdiv(ntB);
   td.ntAB = make_fastdiv(ntA * ntB);
   td.ntiles = ntA * ntB * nb;
@@ -757,7 +778,7 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     tp.ntB = make_fastdiv(pB);
     tp.ntAB = make_fastdiv(pA * pB);
     tp.ntiles = pA * pB * nb;
-    uint64_t g = tp.ntiles;
+    uint64_t g = tp.ntiles / loop_n;
     if (g > kMaxGrid) g = kMaxGrid;
     if (es == 2)
       k_transpose_pk<uint16_t, BM_PK16_TA, BM_PK16_TB, BM_PK16_NT><<<(int)g, BM_PK16_NT, 0, st>>>((const uint16_t *)src,
@@ -768,10 +789,10 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     return BM_OK;
   }
   switch (es) {
-    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, false, st);
-    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, false, st);
-    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, fused, st);
-    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, fused, st);
+    case 1: return launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, false, st, loop_n);
+    case 2: return launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, false, st, loop_n);
+    case 4: return launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, fused, st, loop_n);
+    case 8: return launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, fused, st, loop_n);
     default: break;
   }
   bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);
