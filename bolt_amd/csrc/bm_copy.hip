@@ -81,6 +81,9 @@ constexpr int kThreads = 256;
 #ifndef BM_TR_PAGEORDER
 #define BM_TR_PAGEORDER 0  // transpose: batch dims ordered by max(|src stride|, |dst stride|), smallest fastest (A/B knob)
 #endif
+#ifndef BM_TR_XCD
+#define BM_TR_XCD 0  // transpose: the blocks one XCD runs take a contiguous eighth of the tiles (A/B knob)
+#endif
 #ifndef BM_TR_LOOP
 #define BM_TR_LOOP 0  // transpose: each block walks the batch dim that is page-local on both sides, if >= this many blocks remain (0 = off; A/B knob)
 #endif
@@ -173,6 +176,7 @@ struct TransDesc {
   // long tile rows.
   FastDiv Lb1, La1;
   int64_t sb2, da2;
+  uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (BM_TR_XCD)
 };
 
 // TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
@@ -218,9 +222,10 @@ __global__ void __launch_bounds__(kThreads)
   const int ia = tx * VA;
   const int ib = ux * VB;
 
-  for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
+  for (uint64_t t0 = blockIdx.x; t0 < d.ntiles; t0 += gridDim.x) {
     // consecutive blocks walk dim b (the destination-contiguous one): their
     // stores land side by side in the same destination rows (+9% measured)
+    const uint64_t t = d.xcd8 ? (t0 % 8) * d.xcd8 + t0 / 8 : t0;
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
@@ -610,6 +615,19 @@ struct Tile { int ta, tb; };
 constexpr Tile kTiles1[] = {{128, 256}, {128, 128}, {64, 64}, {256, 64}, {64, 256}};
 constexpr Tile kTiles2[] = {{128, 256}, {64, 256}, {64, 64}, {128, 64}, {256, 32}, {32, 256}};
 constexpr Tile kTiles4[] = {{64, 256}, {32, 256}, {64, 64}, {64, 128}, {128, 32}, {256, 16}, {16, 256}, {32, 64}};
+#ifndef BM_T8_FUSE512
+// f64 with 512-B destination rows whose source rows are at most this many
+// bytes apart (C5 transpose(2,0,4,1,3)): fuse b with its continuation and use
+// BM_T8_FTA x BM_T8_FTB tiles, 1-KiB write segments: +5% (2.798 -> 2.657 ms);
+// with far-apart source rows (C5 .T) fusing loses 5-20% (profiles/r02_ab_f512.log)
+#define BM_T8_FUSE512 4096
+#endif
+#ifndef BM_T8_FTA
+#define BM_T8_FTA 32
+#endif
+#ifndef BM_T8_FTB
+#define BM_T8_FTB 128
+#endif
 #ifndef BM_T8_SQUARE
 #define BM_T8_SQUARE 0  // f64: 64x64 tiles ahead of 32x64 on equal cost (512-B source segments; A/B knob)
 #endif
@@ -637,6 +655,9 @@ int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool 
   } else {
     BM_TILE(32, 256) BM_TILE(16, 256) BM_TILE(32, 64) BM_TILE(64, 64) BM_TILE(64, 32) BM_TILE(128, 16)
     BM_TILE(16, 128)
+#if BM_T8_FUSE512
+    BM_TILE(BM_T8_FTA, BM_T8_FTB)
+#endif
   }
 #undef BM_TILE
   bm_set_error("bm_copy_strided: no transpose tile %dx%d for %d-byte elements", tl.ta, tl.tb, (int)sizeof(T));
@@ -692,16 +713,18 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   // destination (ds == Lb) and a with the dim that continues it in the source
   // (ss == La), so tile rows stay >= 512 B / 256 B (C3 .T: 128-B source rows,
   // +21%, profiles/r01_ab_fuse.log).
-  bool fused = false;
+  bool fused = false, fused512 = false;
   if (BM_FUSE && allow_fuse && es >= 4 && aligned(src, 16) && aligned(dst, 16)) {
     auto take = [&](bool want_b) -> int {
       for (int k = 0; k < (int)batch.size(); ++k)
         if (want_b ? batch[k].ds == td.Lb : batch[k].ss == td.La) return k;
       return -1;
     };
-    if (td.Lb * es < 512) {  // (C5's 512-B rows: fusing measured -10%, profiles/r01_ab_fuse.log)
+    const bool f512 = BM_T8_FUSE512 && es == 8 && td.Lb * es == 512 && std::llabs(td.sb) * es <= BM_T8_FUSE512;
+    if (td.Lb * es < 512 || f512) {
       const int k = take(true);
       if (k >= 0) {
+        fused512 = f512;
         td.sb2 = batch[k].ss;
         td.Lb *= batch[k].n;
         batch.erase(batch.begin() + k);
@@ -727,7 +750,8 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
       return std::max(std::llabs(x.ss), std::llabs(x.ds)) > std::max(std::llabs(y.ss), std::llabs(y.ds));
     });
   }
-  const Tile tl = pick_tile(td.La, td.Lb, es);
+  Tile tl = pick_tile(td.La, td.Lb, es);
+  if (fused512) tl = Tile{BM_T8_FTA, BM_T8_FTB};
   const int TA = tl.ta, TB = tl.tb;
   const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);
   const uint64_t ntB = (uint64_t)((td.Lb + TB - 1) / TB);
@@ -759,6 +783,7 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   td.ntB = make_fastdiv(ntB);
   td.ntAB = make_fastdiv(ntA * ntB);
   td.ntiles = ntA * ntB * nb;
+  td.xcd8 = (BM_TR_XCD && td.ntiles % 8 == 0 && td.ntiles / loop_n <= kMaxGrid && loop_n == 1) ? td.ntiles / 8 : 0;
   // 16-B vectors when every source row start (dims other than a) and every
   // destination row start (dims other than b) is 16-B aligned.
   bool va = aligned(src, 16), vb = aligned(dst, 16);

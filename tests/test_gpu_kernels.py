@@ -87,6 +87,10 @@ def test_permute_all_perms_4d(dtype):
     ((12, 20, 36), (2, 0, 1)),
     ((4, 8, 12, 16, 20), (4, 3, 2, 1, 0)),
     ((16, 16, 16, 16), (2, 3, 0, 1)),
+    # float64 with 512-B destination rows read from nearby source rows: fused
+    # with the continuation, 32 x 128 tiles, a ragged last tile (BM_T8_FUSE512)
+    ((5, 3, 7, 64, 64), (2, 0, 4, 1, 3)),
+    ((6, 64, 5, 64), (2, 0, 3, 1)),
 ])
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64, np.complex128])
 def test_permute_shapes(shape, perm, dtype):
