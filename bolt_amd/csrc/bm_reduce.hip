@@ -36,7 +36,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: grid * block threads < 2^32
 #ifndef BM_COLS_UNROLL
-#define BM_COLS_UNROLL 4  // rows in flight per lane in the column reductions (A/B knob)
+#define BM_COLS_UNROLL 8  // rows in flight per lane in the column reductions: 8 over 4 +1.2-1.4% on the 64 GiB target mean / std and C2-shape columns, 2 -4-8% (profiles/r02_ab_cols.log)
 #endif
 #ifndef BM_COLS_BLOCKS
 #define BM_COLS_BLOCKS 2048  // split R over blocks below this many column tiles (A/B knob)

@@ -178,6 +178,8 @@ OPS = {
     "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
     "t64_mean_cols": lambda: Reduce(0, 1, 4096, 2097152, np.float32, np.float32),
     "t64_std_cols": lambda: Reduce(2, 1, 4096, 2097152, np.float32, np.float32),
+    "t64f_mean_cols": lambda: Reduce(0, 1, 8192, 2097152, np.float32, np.float32),
+    "t64f_std_cols": lambda: Reduce(2, 1, 8192, 2097152, np.float32, np.float32),
     "c4_var_cols": lambda: Reduce(1, 1, 2000, 1024 * 1024, np.uint16, np.float64),
     "c4_var_full": lambda: Reduce(1, 1, 10000, 1024 * 1024, np.uint16, np.float64),
     "u16_var_rows": lambda: Reduce(1, 1024 * 1024, 2000, 1, np.uint16, np.float64),
