@@ -628,6 +628,15 @@ constexpr Tile kTiles4[] = {{64, 256}, {32, 256}, {64, 64}, {64, 128}, {128, 32}
 #ifndef BM_T8_FTB
 #define BM_T8_FTB 128
 #endif
+#ifndef BM_T8_FUSEA
+#define BM_T8_FUSEA 0  // f64 with 512-B source rows far apart (C5 .T): fuse a with its source continuation, BM_T8_FATA x BM_T8_FATB tiles (A/B knob)
+#endif
+#ifndef BM_T8_FATA
+#define BM_T8_FATA 128
+#endif
+#ifndef BM_T8_FATB
+#define BM_T8_FATB 64
+#endif
 #ifndef BM_T8_SQUARE
 #define BM_T8_SQUARE 0  // f64: 64x64 tiles ahead of 32x64 on equal cost (512-B source segments; A/B knob)
 #endif
@@ -657,6 +666,9 @@ int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool 
     BM_TILE(16, 128)
 #if BM_T8_FUSE512
     BM_TILE(BM_T8_FTA, BM_T8_FTB)
+#endif
+#if BM_T8_FUSEA
+    BM_TILE(BM_T8_FATA, BM_T8_FATB)
 #endif
   }
 #undef BM_TILE
@@ -713,7 +725,7 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   // destination (ds == Lb) and a with the dim that continues it in the source
   // (ss == La), so tile rows stay >= 512 B / 256 B (C3 .T: 128-B source rows,
   // +21%, profiles/r01_ab_fuse.log).
-  bool fused = false, fused512 = false;
+  bool fused = false, fused512 = false, fusedA = false;
   if (BM_FUSE && allow_fuse && es >= 4 && aligned(src, 16) && aligned(dst, 16)) {
     auto take = [&](bool want_b) -> int {
       for (int k = 0; k < (int)batch.size(); ++k)
@@ -731,9 +743,11 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
         fused = true;
       }
     }
-    if (td.La * es < 256) {
+    const bool fa = BM_T8_FUSEA && es == 8 && td.La * es == 512 && std::llabs(td.sb) * es > 4096 && !fused;
+    if (td.La * es < 256 || fa) {
       const int k = take(false);
       if (k >= 0) {
+        fusedA = fa;
         td.da2 = batch[k].ds;
         td.La *= batch[k].n;
         batch.erase(batch.begin() + k);
@@ -752,6 +766,7 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   }
   Tile tl = pick_tile(td.La, td.Lb, es);
   if (fused512) tl = Tile{BM_T8_FTA, BM_T8_FTB};
+  if (fusedA) tl = Tile{BM_T8_FATA, BM_T8_FATB};
   const int TA = tl.ta, TB = tl.tb;
   const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);
   const uint64_t ntB = (uint64_t)((td.Lb + TB - 1) / TB);

@@ -697,12 +697,14 @@ class BoltArrayMI355X(BoltArray):
             else:
                 out_dtype = stat_dtype(self._dtype, out_shape)
             perm, O, R, I = reduce_layout(lshape, axset)
+            loc_out = tuple(lshape[i] for i in kept)
             plan = (axset, kept, out_shape, out_dtype, dtype_code(self._dtype), dtype_code(out_dtype),
-                    perm, O, R, I, int(np.prod(lshape, dtype=np.int64)))
+                    perm, O, R, I, int(np.prod(lshape, dtype=np.int64)), loc_out,
+                    int(np.prod(loc_out, dtype=np.int64)))
             if len(_REDUCE_PLANS) > 4096:
                 _REDUCE_PLANS.clear()
             _REDUCE_PLANS[pkey] = plan
-        axset, kept, out_shape, out_dtype, code, ocode, perm, O, R, I, nloc = plan
+        axset, kept, out_shape, out_dtype, code, ocode, perm, O, R, I, nloc, loc_out, nout = plan
         be = self._backend
         dev = self._data.device
         es = self._dtype.itemsize
@@ -715,8 +717,6 @@ class BoltArrayMI355X(BoltArray):
 
         if ctx.world_size == 1 or 0 not in axset:
             # every output lives on this rank (or this rank's slab of them)
-            loc_out = tuple(lshape[i] for i in kept)
-            nout = int(np.prod(loc_out, dtype=np.int64))
             host = host_result(be, nout * out_dtype.itemsize, dev) if ctx.world_size == 1 and nloc else None
             if host is not None:
                 # the kernel stores the result into page-locked host memory
@@ -871,7 +871,10 @@ class BoltArrayMI355X(BoltArray):
 
     def _nrecords(self, axis):
         """Records the reduction sees after _align: the product of the reduced extents."""
-        return int(np.prod([self._shape[int(a)] for a in axis], dtype=np.int64))
+        n = 1
+        for a in axis:
+            n *= int(self._shape[int(a)])
+        return n
 
     def mean(self, axis=None, keepdims=False):
         """Mean over ``axis`` (array.py:336-349)."""

@@ -91,6 +91,12 @@ def test_permute_all_perms_4d(dtype):
     # with the continuation, 32 x 128 tiles, a ragged last tile (BM_T8_FUSE512)
     ((5, 3, 7, 64, 64), (2, 0, 4, 1, 3)),
     ((6, 64, 5, 64), (2, 0, 3, 1)),
+    # short rows whose fastest row dim strides the source by >= 64 KiB: the
+    # rowcopy walks 16x16 diagonal tiles (Diag16), with and without outer dims,
+    # and a row dim that is not a multiple of 16 (row order)
+    ((64, 32, 64, 8), (1, 2, 0, 3)),
+    ((32, 4, 16, 32, 16), (1, 2, 3, 0, 4)),
+    ((48, 20, 40, 8), (1, 2, 0, 3)),
 ])
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64, np.complex128])
 def test_permute_shapes(shape, perm, dtype):
