@@ -50,6 +50,15 @@ constexpr int kThreads = 256;
 #ifndef BM_PK16_NT
 #define BM_PK16_NT 1024
 #endif
+#ifndef BM_PK8_PIPE
+// packed transposes, software-pipelined blocks (k_transpose_pkp), this many
+// per CU (0 = off): uint8 .T +9.8%; uint16 +1-2% on .T but -3% on a 2-D
+// transpose, so off (profiles/r02_ab_pkpipe.log)
+#define BM_PK8_PIPE 1
+#endif
+#ifndef BM_PK16_PIPE
+#define BM_PK16_PIPE 0
+#endif
 #ifndef BM_PK8_TA
 #define BM_PK8_TA 128
 #define BM_PK8_TB 512
@@ -358,6 +367,110 @@ __global__ void __launch_bounds__(NT)
 
     T *q = dst + dof + b0 + a0 * d.da;
     const int ib = ux * 4 * P;  // first element of this lane's 16 B along b
+    const bool fullB = (b0 + ib + 4 * P <= d.Lb);
+#pragma unroll
+    for (int it = 0; it < NS; ++it) {
+      const int ra = uy + it * RPB;
+      if (a0 + ra < d.La) {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = tile[ux * 4 + k][ra];
+        T *p = q + (int64_t)ra * d.da + ib;
+        if (fullB) {
+          typedef typename VecB<16>::t V16;
+          V16 x;
+          __builtin_memcpy(&x, w, 16);
+          __builtin_nontemporal_store(x, reinterpret_cast<V16 *>(p));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4 * P; ++e)
+            if (b0 + ib + e < d.Lb) p[e] = (T)(w[e / P] >> ((e % P) * BITS));
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Software-pipelined packed transpose: a block walks tiles t, t + grid, ... and
+// issues the global loads of its next tile before the LDS reads and global
+// stores of the current one, so HBM reads stay in flight through the store
+// phase (the 128-KiB u16 tile leaves room for one block per CU, whose load and
+// store phases would otherwise alternate).  Same tile layout as k_transpose_pk.
+template <typename T, int TA, int TB, int NT = kThreads>
+__global__ void __launch_bounds__(NT)
+    k_transpose_pkp(const T *__restrict__ src, T *__restrict__ dst, TransDesc d) {
+  constexpr int P = 4 / (int)sizeof(T);
+  constexpr int VA = 16 / (int)sizeof(T);
+  constexpr int TBW = TB / P;
+  constexpr int NVA = TA / VA;
+  constexpr int RGA = NT / NVA;
+  constexpr int NL = TBW / RGA;
+  constexpr int NVB = TBW / 4;
+  constexpr int RPB = NT / NVB;
+  constexpr int NS = TA / RPB;
+  constexpr int BITS = 8 * (int)sizeof(T);
+  static_assert(NL >= 1 && TBW % RGA == 0 && NS >= 1 && TA % RPB == 0, "tile too small for the thread layout");
+  static_assert(NL * P * 4 <= 64, "loads in flight exceed the register budget");
+  __shared__ uint32_t tile[TBW][TA + 1];
+  const int tx = threadIdx.x % NVA, ty = threadIdx.x / NVA;
+  const int ux = threadIdx.x % NVB, uy = threadIdx.x / NVB;
+  const int ia = tx * VA;
+
+  T v[NL][P][VA];
+  auto coords = [&](uint64_t t, int64_t &a0, int64_t &b0, int64_t &so, int64_t &dof) {
+    const uint64_t bt = fd_div(t, d.ntAB);
+    const uint64_t rem = t - bt * d.ntAB.d;
+    const uint64_t ta = fd_div(rem, d.ntB);
+    const uint64_t tb = rem - ta * d.ntB.d;
+    decomp2(bt, d.batch, so, dof);
+    a0 = (int64_t)ta * TA;
+    b0 = (int64_t)tb * TB;
+  };
+  auto load = [&](uint64_t t) {
+    int64_t a0, b0, so, dof;
+    coords(t, a0, b0, so, dof);
+    const T *s = src + so + a0 + b0 * d.sb;
+    const bool fullA = (a0 + ia + VA <= d.La);
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int wr = ty + it * RGA;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int rb = wr * P + j;
+        const T *p = s + ia + (int64_t)rb * d.sb;
+        if (b0 + rb < d.Lb && fullA) {
+          vload_nt<T, VA>(p, v[it][j]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < VA; ++k) v[it][j][k] = (b0 + rb < d.Lb && a0 + ia + k < d.La) ? p[k] : T(0);
+        }
+      }
+    }
+  };
+
+  uint64_t t = blockIdx.x;
+  if (t < d.ntiles) load(t);
+  for (; t < d.ntiles; t += gridDim.x) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int wr = ty + it * RGA;
+#pragma unroll
+      for (int k = 0; k < VA; ++k) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) w |= (uint32_t)v[it][j][k] << (j * BITS);
+        tile[wr][ia + k] = w;
+      }
+    }
+    __syncthreads();
+    const uint64_t tn = t + gridDim.x;
+    if (tn < d.ntiles) load(tn);  // in flight during this tile's stores
+
+    int64_t a0, b0, so, dof;
+    coords(t, a0, b0, so, dof);
+    T *q = dst + dof + b0 + a0 * d.da;
+    const int ib = ux * 4 * P;
     const bool fullB = (b0 + ib + 4 * P <= d.Lb);
 #pragma unroll
     for (int it = 0; it < NS; ++it) {
@@ -820,6 +933,18 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     tp.ntiles = pA * pB * nb;
     uint64_t g = tp.ntiles / loop_n;
     if (g > kMaxGrid) g = kMaxGrid;
+    const int pipe = es == 2 ? BM_PK16_PIPE : BM_PK8_PIPE;
+    if (pipe) {
+      const uint64_t cap = 256ull * pipe;  // MI355X: 256 CUs
+      if (g > cap) g = cap;
+      if (es == 2)
+        k_transpose_pkp<uint16_t, BM_PK16_TA, BM_PK16_TB, BM_PK16_NT><<<(int)g, BM_PK16_NT, 0, st>>>(
+            (const uint16_t *)src, (uint16_t *)dst, tp);
+      else
+        k_transpose_pkp<uint8_t, BM_PK8_TA, BM_PK8_TB, BM_PK8_NT><<<(int)g, BM_PK8_NT, 0, st>>>(
+            (const uint8_t *)src, (uint8_t *)dst, tp);
+      return BM_OK;
+    }
     if (es == 2)
       k_transpose_pk<uint16_t, BM_PK16_TA, BM_PK16_TB, BM_PK16_NT><<<(int)g, BM_PK16_NT, 0, st>>>((const uint16_t *)src,
                                                                                  (uint16_t *)dst, tp);
