@@ -469,7 +469,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": "%s (bm_permute) for the %s" % (ROOFLINE_KERNEL[cfg], ops[0][0]) if world == 1 else
-                          "swap = pack + RCCL all_to_all + unpack (per rank)",
+                          "swap = pack + all_to_all + unpack (per rank)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
@@ -482,18 +482,20 @@ def main():
         }
         if world > 1:
             G = world
+            xport = "RCCL" if backend == "nccl" else "%s (host-staged rehearsal)" % backend
             n_rank = ops[0][2] / 2                        # bytes held per rank
             payload = n_rank * (G - 1) / G                # bytes each rank sends to its peers
             ex = phases.get("exchange")
             if ex:  # the swap across GPUs: pipelined pack -> RCCL all-to-all -> unpack
-                line["roofline"].update({"kernel": "swap exchange per rank (k_transpose pack + RCCL "
-                                                   "all_to_all + k_rowcopy unpack, pipelined)",
+                line["roofline"].update({"kernel": "swap exchange per rank (k_transpose pack + %s "
+                                                   "all_to_all + k_rowcopy unpack, pipelined)" % xport,
                                          "achieved": round(2 * n_rank / (ex / 1e3) / 1e9, 1),
                                          "avg_ms": round(ex, 4), "bytes_per_launch": int(2 * n_rank)})
                 line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
             a2a = phases.get("exchange")
             peak = (G - 1) * XGMI_LINK_GBPS
-            line["xgmi"] = {"op": "RCCL send/recv group (bm_alltoallv) inside the pipelined swap exchange "
+            line["xgmi"] = {"op": ("RCCL send/recv group (bm_alltoallv)" if backend == "nccl" else
+                                   "%s all_to_all" % xport) + " inside the pipelined swap exchange "
                                   "(achieved = peer payload / whole exchange time: a lower bound)",
                             "payload_bytes_per_rank": int(payload),
                             "avg_ms": round(a2a, 4) if a2a else None,
