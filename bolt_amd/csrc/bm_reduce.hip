@@ -985,6 +985,94 @@ __global__ void __launch_bounds__(kThreads)
   }
 }
 
+// Few outputs, many parts (axis=None statistics: one output from hundreds of
+// chunk states): one block per output.  Thread t merges the contiguous run of
+// parts [t*L, (t+1)*L) in order, then the 256 partial states merge in a fixed
+// binary tree through LDS (thread j absorbs j + s): deterministic, and a
+// serial chain of hundreds of dependent loads and divisions becomes ~L + 8.
+struct PartState {
+  double n, m, q;
+  uint64_t u;
+  int64_t s1, cnt;
+  uint64_t s2;
+  int any;
+};
+
+template <int MODE, typename T>
+__device__ __forceinline__ void merge_state(PartState &a, const PartState &b, bool int_sums) {
+  if (!b.any) return;
+  if (!a.any) {
+    a = b;
+    return;
+  }
+  if (MODE == M_MOM && int_sums) {
+    a.s1 += b.s1; a.s2 += b.s2; a.cnt += b.cnt;
+  } else if (MODE == M_MEAN || MODE == M_MOM) {
+    chan(a.n, a.m, a.q, b.n, b.m, b.q, MODE == M_MOM);
+  } else if (facc_mode<MODE>()) {
+    a.m = fop<MODE>(a.m, b.m);
+    a.n += b.n;
+  } else {
+    a.u = bop<T, MODE>(a.u, b.u);
+  }
+}
+
+template <int MODE, typename T>
+__global__ void __launch_bounds__(kThreads)
+    k_red_combine_blk(const double *__restrict__ p0, const double *__restrict__ p1, CombDesc d, Sink sk) {
+  __shared__ PartState sm[kThreads];
+  const int64_t e = blockIdx.x;
+  const bool int_sums = MODE == M_MOM && d.int_sums;
+  const int64_t L = (d.nparts + kThreads - 1) / kThreads;
+  const int64_t p_lo = (int64_t)threadIdx.x * L, p_hi = min(d.nparts, p_lo + L);
+  PartState st{};
+  for (int64_t p = p_lo; p < p_hi; ++p) {
+    const int64_t cnt = d.explicit_counts ? d.counts[p] : min(d.R, (p + 1) * d.rchunk) - p * d.rchunk;
+    if (cnt <= 0) continue;
+    const int64_t at = p * d.part_stride + e;
+    PartState b{};
+    b.any = 1;
+    b.n = (double)cnt;
+    if (int_sums) {
+      b.s1 = reinterpret_cast<const int64_t *>(p0)[at];
+      b.s2 = reinterpret_cast<const uint64_t *>(p1)[at];
+      b.cnt = cnt;
+    } else if (MODE == M_MEAN || MODE == M_MOM) {
+      b.m = p0[at];
+      b.q = (MODE == M_MOM) ? p1[at] : 0.0;
+    } else if (facc_mode<MODE>()) {
+      b.m = p0[at];
+    } else {
+      b.u = ((const uint64_t *)p0)[at];
+    }
+    merge_state<MODE, T>(st, b, int_sums);
+  }
+  sm[threadIdx.x] = st;
+  for (int s = 1; s < kThreads; s <<= 1) {
+    __syncthreads();
+    if ((threadIdx.x & (2 * s - 1)) == 0) {
+      PartState a = sm[threadIdx.x];
+      merge_state<MODE, T>(a, sm[threadIdx.x + s], int_sums);
+      sm[threadIdx.x] = a;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const PartState r = sm[0];
+  if constexpr (MODE == M_MOM) {
+    if (int_sums) {
+      double mean, m2;
+      int_moments((uint64_t)r.cnt, r.s1, r.s2, mean, m2);
+      emit_mom(sk, e, e, 1, (double)r.cnt, mean, m2, 0.0);
+      return;
+    }
+    const double P = d.pivots ? p1[d.nparts * d.part_stride + e] : 0.0;
+    emit_mom(sk, e, e, 1, r.n, r.m, r.q, P);
+  } else {
+    emit<MODE>(sk, e, r.n, r.m, r.q, r.u);
+  }
+}
+
 // ------------------------------------------------------------------ host --
 int dtype_size(int dt) {
   switch (dt) {
@@ -1231,21 +1319,34 @@ int launch_main(int mode, int dt, const RedPlan &p, const void *src, int64_t O, 
   }
 }
 
+#ifndef BM_COMB_BLK
+#define BM_COMB_BLK 1  // block-per-output combine for few outputs and many parts (0 = off; A/B knob)
+#endif
+bool comb_blk(const CombDesc &cd) { return BM_COMB_BLK && cd.nout <= 1024 && cd.nparts >= 8; }
+
+template <int MODE, typename T>
+void launch_combine_k(int g, const double *p0, const double *p1, const CombDesc &cd, Sink sk, hipStream_t st) {
+  if (comb_blk(cd))
+    k_red_combine_blk<MODE, T><<<(int)cd.nout, kThreads, 0, st>>>(p0, p1, cd, sk);
+  else
+    k_red_combine<MODE, T><<<g, kThreads, 0, st>>>(p0, p1, cd, sk);
+}
+
 template <int MODE>
 void launch_combine_m(int dt, int g, const double *p0, const double *p1, const CombDesc &cd, Sink sk,
                       hipStream_t st) {
   switch (dt) {  // only max/min look at the element type
-    case BM_BOOL: case BM_U8: k_red_combine<MODE, uint8_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_I8: k_red_combine<MODE, int8_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_U16: k_red_combine<MODE, uint16_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_I16: k_red_combine<MODE, int16_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_U32: k_red_combine<MODE, uint32_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_I32: k_red_combine<MODE, int32_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_U64: k_red_combine<MODE, uint64_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_I64: k_red_combine<MODE, int64_t><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_F16: k_red_combine<MODE, _Float16><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case BM_F32: k_red_combine<MODE, float><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    default: k_red_combine<MODE, double><<<g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case BM_BOOL: case BM_U8: launch_combine_k<MODE, uint8_t>(g, p0, p1, cd, sk, st); break;
+    case BM_I8: launch_combine_k<MODE, int8_t>(g, p0, p1, cd, sk, st); break;
+    case BM_U16: launch_combine_k<MODE, uint16_t>(g, p0, p1, cd, sk, st); break;
+    case BM_I16: launch_combine_k<MODE, int16_t>(g, p0, p1, cd, sk, st); break;
+    case BM_U32: launch_combine_k<MODE, uint32_t>(g, p0, p1, cd, sk, st); break;
+    case BM_I32: launch_combine_k<MODE, int32_t>(g, p0, p1, cd, sk, st); break;
+    case BM_U64: launch_combine_k<MODE, uint64_t>(g, p0, p1, cd, sk, st); break;
+    case BM_I64: launch_combine_k<MODE, int64_t>(g, p0, p1, cd, sk, st); break;
+    case BM_F16: launch_combine_k<MODE, _Float16>(g, p0, p1, cd, sk, st); break;
+    case BM_F32: launch_combine_k<MODE, float>(g, p0, p1, cd, sk, st); break;
+    default: launch_combine_k<MODE, double>(g, p0, p1, cd, sk, st); break;
   }
 }
 
@@ -1255,17 +1356,17 @@ int launch_combine(int mode, int dt, const double *p0, const double *p1, const C
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
   switch (mode) {
-    case M_MEAN: k_red_combine<M_MEAN, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_MOM: k_red_combine<M_MOM, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_FSUM: k_red_combine<M_FSUM, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_FPROD: k_red_combine<M_FPROD, double><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_ISUM: k_red_combine<M_ISUM, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_IPROD: k_red_combine<M_IPROD, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_OR: k_red_combine<M_OR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_LAND: k_red_combine<M_LAND, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_BAND: k_red_combine<M_BAND, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_BOR: k_red_combine<M_BOR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
-    case M_BXOR: k_red_combine<M_BXOR, uint64_t><<<(int)g, kThreads, 0, st>>>(p0, p1, cd, sk); break;
+    case M_MEAN: launch_combine_k<M_MEAN, double>((int)g, p0, p1, cd, sk, st); break;
+    case M_MOM: launch_combine_k<M_MOM, double>((int)g, p0, p1, cd, sk, st); break;
+    case M_FSUM: launch_combine_k<M_FSUM, double>((int)g, p0, p1, cd, sk, st); break;
+    case M_FPROD: launch_combine_k<M_FPROD, double>((int)g, p0, p1, cd, sk, st); break;
+    case M_ISUM: launch_combine_k<M_ISUM, uint64_t>((int)g, p0, p1, cd, sk, st); break;
+    case M_IPROD: launch_combine_k<M_IPROD, uint64_t>((int)g, p0, p1, cd, sk, st); break;
+    case M_OR: launch_combine_k<M_OR, uint64_t>((int)g, p0, p1, cd, sk, st); break;
+    case M_LAND: launch_combine_k<M_LAND, uint64_t>((int)g, p0, p1, cd, sk, st); break;
+    case M_BAND: launch_combine_k<M_BAND, uint64_t>((int)g, p0, p1, cd, sk, st); break;
+    case M_BOR: launch_combine_k<M_BOR, uint64_t>((int)g, p0, p1, cd, sk, st); break;
+    case M_BXOR: launch_combine_k<M_BXOR, uint64_t>((int)g, p0, p1, cd, sk, st); break;
     case M_MAX: launch_combine_m<M_MAX>(dt, (int)g, p0, p1, cd, sk, st); break;
     case M_FMAX: launch_combine_m<M_FMAX>(dt, (int)g, p0, p1, cd, sk, st); break;
     case M_FMIN: launch_combine_m<M_FMIN>(dt, (int)g, p0, p1, cd, sk, st); break;

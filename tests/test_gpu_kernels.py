@@ -225,6 +225,55 @@ def test_reduce_sum(dtype, O, R, I):
         assert np.all(np.abs(got - truth) <= tol * np.abs(x).astype(np.longdouble).sum(axis=1) + 1e-300)
 
 
+@pytest.mark.parametrize("O,R,I", [(1, 1 << 18, 1), (1, 120000, 6)])
+@pytest.mark.parametrize("dtype", [np.int32, np.uint16, np.float64, np.float32, np.bool_])
+def test_reduce_modes_few_outputs(O, R, I, dtype):
+    """Few outputs from hundreds of chunk states (axis=None-like reductions):
+    every mode through the block-per-output combine (k_red_combine_blk)."""
+    import torch
+    from bolt_amd.mi355x import _lib
+    from bolt_amd.mi355x._ops import dtype_code
+    be = _be()
+    rng = np.random.default_rng(R + I)
+    dt = np.dtype(dtype)
+    if dt == np.bool_:
+        x = rng.random((O, R, I)) < 0.9999
+        x[0, :, 0] = True  # one all-True column
+        stats = {_lib.STAT_LAND: np.logical_and, _lib.STAT_LOR: np.logical_or, _lib.STAT_SUM: np.logical_or,
+                 _lib.STAT_MAX: np.maximum, _lib.STAT_MIN: np.minimum, _lib.STAT_PROD: np.logical_and}
+    elif dt.kind == 'f':
+        x = (1 + 1e-7 * rng.standard_normal((O, R, I))).astype(dt)
+        if I > 1:
+            x[0, 12345, 1] = np.nan  # NaN wins in maximum/minimum, loses in fmax/fmin
+        stats = {_lib.STAT_MAX: np.maximum, _lib.STAT_MIN: np.minimum, _lib.STAT_FMAX: np.fmax,
+                 _lib.STAT_FMIN: np.fmin, _lib.STAT_PROD: np.multiply, _lib.STAT_SUM: np.add}
+    else:
+        info = np.iinfo(dt)
+        x = rng.integers(info.min, info.max, size=(O, R, I), dtype=dt, endpoint=True)
+        stats = {_lib.STAT_MAX: np.maximum, _lib.STAT_MIN: np.minimum, _lib.STAT_PROD: np.multiply,
+                 _lib.STAT_BAND: np.bitwise_and, _lib.STAT_BOR: np.bitwise_or, _lib.STAT_BXOR: np.bitwise_xor,
+                 _lib.STAT_LAND: np.logical_and, _lib.STAT_LOR: np.logical_or, _lib.STAT_SUM: np.add}
+    src = _dev(x)
+    for stat, uf in stats.items():
+        out_dt = np.dtype(bool) if stat in (_lib.STAT_LAND, _lib.STAT_LOR) else dt
+        out = torch.empty(O * I * out_dt.itemsize, dtype=torch.uint8, device="cuda")
+        be.reduce(stat, src, dtype_code(dt), O, R, I, out, dtype_code(out_dt))
+        got = _host(out, out_dt, (O, I))
+        if dt.kind == 'f' and uf in (np.multiply, np.add):
+            truth = uf.reduce(x.astype(np.longdouble), axis=1)
+            tol = 1e-6 if dt == np.float32 else 1e-10
+            nan = np.isnan(truth)
+            assert np.array_equal(np.isnan(got), nan), (stat, got, truth)
+            assert np.all(np.abs(got[~nan] - truth[~nan]) <= tol * np.abs(truth[~nan])), (stat, got, truth)
+        else:
+            want = np.asarray(uf.reduce(x, axis=1, dtype=out_dt) if out_dt != np.bool_ or dt == np.bool_
+                              else uf.reduce(x != 0, axis=1), out_dt)
+            if dt.kind == 'f':
+                assert np.array_equal(got, want, equal_nan=True), (stat, got, want)
+            else:
+                assert got.tobytes() == want.tobytes(), (stat, got, want)
+
+
 def test_reduce_state_and_combine_match_single_pass():
     import torch
     from bolt_amd.mi355x import _lib
