@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <vector>
+#include <dlfcn.h>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 typedef __attribute__((ext_vector_type(2))) double d2;
@@ -129,7 +130,7 @@ __global__ void k_fill(uint64_t* p, uint64_t n) {
     p[i] = i * 0x9E3779B97F4A7C15ull;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int ncu = 0;
   CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   const uint64_t n = 1ull << 30;  // 64^5 elements
@@ -144,9 +145,20 @@ int main() {
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
 
+  // the product library's bm_permute on the same buffers (argv[1]: path to libbolt_mi355x.so)
+  typedef int (*permute_fn)(const void*, void*, int, const int64_t*, const int32_t*, int, void*);
+  permute_fn prod = nullptr;
+  if (argc > 1) {
+    void* h = dlopen(argv[1], RTLD_NOW);
+    if (!h) { printf("dlopen %s: %s\n", argv[1], dlerror()); return 1; }
+    prod = (permute_fn)dlsym(h, "bm_permute");
+  }
+  const int64_t shp[5] = {64, 64, 64, 64, 64};
+  const int32_t prm[5] = {4, 3, 2, 1, 0};
   struct Var { const char* name; int kind; int M; };
   std::vector<Var> vars = {{"base/O0", 0, 0}, {"base/O1", 1, 0}, {"pipe/gs", 2, 0}, {"pipe/8", 3, 8},
                            {"pipe/32", 3, 32}, {"pipe/128", 3, 128}, {"pipe/512", 3, 512}, {"copy", 4, 0}};
+  if (prod) vars.insert(vars.begin() + 1, Var{"product", 5, 0});
   for (int rep = 0; rep < 3; ++rep) {
     for (const Var& v : vars) {
       auto launch = [&]() {
@@ -155,7 +167,10 @@ int main() {
           case 1: k_base<1><<<(int)NT, 256>>>(src, dst); break;
           case 2: k_pipe<0><<<ncu * 8, 256>>>(src, dst, 0); break;
           case 3: k_pipe<1><<<(int)((NT + v.M - 1) / v.M), 256>>>(src, dst, v.M); break;
-          default: k_copy<<<ncu * 64, 256>>>((const f4*)src, (f4*)dst, n * 8 / 16); break;
+          case 4: k_copy<<<ncu * 64, 256>>>((const f4*)src, (f4*)dst, n * 8 / 16); break;
+          default:
+            if (prod(src, dst, 5, shp, prm, 8, nullptr)) { printf("bm_permute failed\n"); exit(1); }
+            break;
         }
       };
       CK(hipMemset(dst, 0, n * 8));
