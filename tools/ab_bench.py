@@ -60,6 +60,12 @@ class Permute(object):
                             len(self.shape), i64(self.shape), i32(self.perm), self.es, stream())
         assert rc == 0, lib.bm_last_error()
 
+    def check(self):
+        """dst == src.permute(perm) byte for byte (torch reference, same element size)."""
+        tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[self.es]
+        ref = self.src.view(tdt).view(self.shape).permute(self.perm).contiguous()
+        return bool(torch.equal(ref.view(-1), self.dst.view(tdt)))
+
 
 class Reduce(object):
     CODES = {np.dtype(np.float32): 10, np.dtype(np.float64): 11, np.dtype(np.uint16): 3}
@@ -194,14 +200,21 @@ def main():
     ap.add_argument("--ops", default=",".join(OPS))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--check", action="store_true", help="compare every library's permute output with torch's")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     for name in a.ops.split(","):
         op = OPS[name]()
         times = [[] for _ in libs]
         for _ in range(2):
-            for lib in libs:
+            for k, lib in enumerate(libs):
                 op(lib)
+                if a.check and hasattr(op, "check") and _ == 0:
+                    op.dst.fill_(0)
+                    op(lib)
+                    torch.cuda.synchronize()
+                    if not op.check():
+                        print("%-14s %-40s OUTPUT MISMATCH" % (name, a.libs[k].split("/")[-1]), flush=True)
         for _ in range(a.rounds):
             for k, lib in enumerate(libs):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
