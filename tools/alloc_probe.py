@@ -21,6 +21,8 @@ from bolt_amd.mi355x import _lib  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--hip-first", action="store_true", help="hipMalloc the raw buffers before torch allocates")
+    ap.add_argument("--cases", default="c5_T,c2_swap")
     args = ap.parse_args()
     lib = _lib.load()
     hip = ctypes.CDLL("libamdhip64.so")
@@ -30,14 +32,21 @@ def main():
     torch.cuda.init()
     st = torch.cuda.current_stream()
     cases = {"c5_T": ((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), 8),
-             "c2_swap": ((2000, 512 * 512), (1, 0), 4)}
+             "c2_swap": ((2000, 512 * 512), (1, 0), 4),
+             "c3_T": ((1024, 256, 256, 32), (3, 2, 1, 0), 4),
+             "c3_swap": ((1024, 256, 256, 32), (1, 2, 0, 3), 4)}
     for name, (shape, perm, es) in cases.items():
+        if name not in args.cases.split(","):
+            continue
         nbytes = int(np.prod(shape)) * es
+        hs, hd = ctypes.c_void_p(), ctypes.c_void_p()
+        if args.hip_first:
+            assert hip.hipMalloc(ctypes.byref(hs), nbytes) == 0 and hip.hipMalloc(ctypes.byref(hd), nbytes) == 0
         ts = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
         td = torch.empty_like(ts)
         ts.fill_(7)
-        hs, hd = ctypes.c_void_p(), ctypes.c_void_p()
-        assert hip.hipMalloc(ctypes.byref(hs), nbytes) == 0 and hip.hipMalloc(ctypes.byref(hd), nbytes) == 0
+        if not args.hip_first:
+            assert hip.hipMalloc(ctypes.byref(hs), nbytes) == 0 and hip.hipMalloc(ctypes.byref(hd), nbytes) == 0
         assert hip.hipMemset(hs, 7, nbytes) == 0
         torch.cuda.synchronize()
         shp = (ctypes.c_int64 * len(shape))(*shape)
@@ -49,7 +58,12 @@ def main():
         als, ald = (gs.value + G - 1) // G * G, (gd.value + G - 1) // G * G
         assert hip.hipMemset(ctypes.c_void_p(als), 7, nbytes) == 0
         torch.cuda.synchronize()
+        # the same carve-out from torch's caching allocator
+        tgs = torch.empty(nbytes + G, dtype=torch.uint8, device="cuda")
+        tgd = torch.empty(nbytes + G, dtype=torch.uint8, device="cuda")
+        tas, tad = (tgs.data_ptr() + G - 1) // G * G, (tgd.data_ptr() + G - 1) // G * G
         bufs = {"torch": (ts.data_ptr(), td.data_ptr()), "hipMalloc": (hs.value, hd.value),
+                "torch_1G": (tas, tad),
                 "t_src/h_dst": (ts.data_ptr(), hd.value), "h_src/t_dst": (hs.value, td.data_ptr()),
                 "hip_1G": (als, ald)}
         print("%s: torch src 0x%x dst 0x%x | hipMalloc src 0x%x dst 0x%x" %
@@ -72,7 +86,7 @@ def main():
             med = float(np.median(v))
             print("%-8s %-12s median %.4f ms  %.1f GB/s  rounds %s" % (name, k, med, 2 * nbytes / med / 1e6,
                                                                      " ".join("%.4f" % x for x in v)), flush=True)
-        del ts, td
+        del ts, td, tgs, tgd
         for p in (hs, hd, gs, gd):
             hip.hipFree(p)
         torch.cuda.empty_cache()
