@@ -90,6 +90,13 @@ constexpr int kThreads = 256;
 #ifndef BM_TR_PAGEORDER
 #define BM_TR_PAGEORDER 0  // transpose: batch dims ordered by max(|src stride|, |dst stride|), smallest fastest (A/B knob)
 #endif
+#ifndef BM_TR_ROT
+// transpose: rotate each a-row of tiles by its a-tile index, so a partial last
+// b-tile (C2: 2000 = 7 x 256 + 208) is not always dispatched to the same XCD
+// (round-robin dispatch: block t runs on XCD t % 8, and with 8 b-tiles the
+// b-tile index IS the XCD).  Same tiles per group of blocks, same locality.
+#define BM_TR_ROT 0
+#endif
 #ifndef BM_TR_XCD
 #define BM_TR_XCD 0  // transpose: the blocks one XCD runs take a contiguous eighth of the tiles (A/B knob)
 #endif
@@ -238,7 +245,11 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
-    const uint64_t tb = rem - ta * d.ntB.d;
+    uint64_t tb = rem - ta * d.ntB.d;
+    if (BM_TR_ROT) {
+      tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
+      if (tb >= d.ntB.d) tb -= d.ntB.d;
+    }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
@@ -329,7 +340,11 @@ __global__ void __launch_bounds__(NT)
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
-    const uint64_t tb = rem - ta * d.ntB.d;
+    uint64_t tb = rem - ta * d.ntB.d;
+    if (BM_TR_ROT) {
+      tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
+      if (tb >= d.ntB.d) tb -= d.ntB.d;
+    }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
@@ -528,7 +543,11 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
-    const uint64_t tb = rem - ta * d.ntB.d;
+    uint64_t tb = rem - ta * d.ntB.d;
+    if (BM_TR_ROT) {
+      tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
+      if (tb >= d.ntB.d) tb -= d.ntB.d;
+    }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * kRunTB;

@@ -2,8 +2,11 @@
 net permutations of swap/transpose, reduction layouts and result dtypes.
 
 Everything here is integer/shape arithmetic that decides what the HIP kernels
-do; no data is touched.  Each function restates (not copies) the reference
-semantics it cites, including the quirks a drop-in must keep.
+do; no data is touched.  Each function restates the reference semantics it
+cites, including the quirks a drop-in must keep.  The chunk-plan functions
+(getplan, getslices, removepad_slices) follow chunk.py:434-618 step by step,
+because their integer results must be identical to the reference's; the
+geometry, permutation and reduction-layout code below them is new.
 """
 import functools
 from itertools import product
