@@ -19,7 +19,7 @@ import numpy as np
 class MI355XContext(object):
 
     _default = None
-    _ncomm = 0  # communicators created by this process (names their rendezvous keys)
+    _ncomm = {}  # communicators created by this process, per rank set (names their rendezvous keys)
 
     def __init__(self, device=None, group=None):
         import torch
@@ -58,8 +58,7 @@ class MI355XContext(object):
         import torch.distributed as dist
         from bolt_amd.mi355x import _lib
         lib = _lib.load()
-        MI355XContext._ncomm += 1
-        key = "bolt_amd/rccl_id/%d" % MI355XContext._ncomm
+        key = self._comm_key(dist.get_process_group_ranks(self.group or dist.group.WORLD))
         uid = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
         store = dist.distributed_c10d._get_default_store()
         if self.rank == 0:
@@ -72,6 +71,18 @@ class MI355XContext(object):
         _lib.check(lib.bm_comm_init(ctypes.byref(comm), self.world_size, uid, self.rank), "bm_comm_init")
         self.comm = comm.value
         self.comm_stream = torch.cuda.Stream(self.device)
+
+    @classmethod
+    def _comm_key(cls, ranks):
+        """Rendezvous key of the next communicator over ``ranks`` (global ranks).
+
+        Counted per rank set, so processes that open contexts over different
+        subgroups in different orders still agree on every key (a single
+        process-wide counter would hand a rank the id of another group)."""
+        ranks = tuple(int(r) for r in ranks)
+        n = cls._ncomm.get(ranks, 0) + 1
+        cls._ncomm[ranks] = n
+        return "bolt_amd/rccl_id/%s/%d" % (",".join(map(str, ranks)), n)
 
     def close(self):
         """Release the RCCL communicator (before the process group is destroyed)."""
