@@ -331,16 +331,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (not the measured configuration): several ranks on one
-    # GPU over gloo, exchanges staged through the host
+    # GPU over gloo, exchanges staged through the host by the test executor
+    # of tests/cpu_backend.py (RCCL refuses two ranks on one GPU)
     backend = os.environ.get("BOLT_AMD_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("BOLT_AMD_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            # gloo for the host-side barrier / timing max / metadata, nccl only
+            # as the group's device backend: no device_id, no eager torch RCCL
+            # communicator -- the one RCCL communicator per rank is the
+            # library's (MI355XContext, bm_comm_init through the group's store)
+            dist.init_process_group("cpu:gloo,cuda:nccl")
         else:
             dist.init_process_group(backend)
+            sys.path.insert(0, os.path.join(HERE, "tests"))
+            import cpu_backend
+            cpu_backend.install_host_staged_gpu()
 
     import bolt_amd as bolt
     from bolt_amd import MI355XContext
@@ -348,8 +356,9 @@ def main():
     assert ctx.world_size == world
 
     def barrier():
+        torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            dist.barrier()  # over gloo (host)
         torch.cuda.synchronize()
 
     def measure(cfg, steps, warmup):
@@ -430,7 +439,7 @@ def main():
                 rccl_ms = float(np.sum([a.elapsed_time(z) for a, z in bdist.PROFILE["rccl"]])) / steps
             bdist.PROFILE = None
         if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            t = torch.tensor([elapsed], dtype=torch.float64)  # host tensor: over gloo
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
 
@@ -463,8 +472,9 @@ def main():
             "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
             "config": {"workload": desc, "global_shape": list(gshape), "split": split,
                        "parallelism": "dp%d (records sharded on the leading key axis)" % world,
-                       "collectives": "RCCL via libbolt_mi355x (bm_alltoallv / bm_allgatherv)" if backend == "nccl" or world == 1
-                                      else "%s, host-staged (one-GPU rehearsal, not a measurement)" % backend,
+                       "collectives": ("none (single GPU)" if world == 1 else
+                                       "RCCL via libbolt_mi355x (bm_alltoallv / bm_allgatherv)" if ctx.comm
+                                       else "%s, host-staged (one-GPU rehearsal, not a measurement)" % backend),
                        "bytes_per_step": {k: int(v) for k, v in per.items()}},
             "roofline": {
                 "bound": "hbm",

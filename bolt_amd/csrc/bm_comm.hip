@@ -19,11 +19,13 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 
 namespace {
 
@@ -121,7 +123,40 @@ int nccl_check(ncclResult_t r, const char *who, const char *what) {
 struct Comm {
   ncclComm_t comm;
   int rank, world;
+  bool aborted;      // ncclCommAbort has run: the handle is gone, every call fails
+  char why[256];     // what aborted it
 };
+
+// The communicator after a failure: abort it once (RCCL kernels still in
+// flight see the abort flag and exit, so streams drain instead of hanging)
+// and remember why.
+int comm_fail(Comm *c, const char *who, const char *why) {
+  if (!c->aborted) {
+    c->aborted = true;
+    std::snprintf(c->why, sizeof(c->why), "%s", why);
+    if (g_rccl.commAbort) g_rccl.commAbort(c->comm);
+  }
+  bm_set_error("%s: communicator aborted: %s", who, c->why);
+  return BM_E_COMM;
+}
+
+// BM_OK, or abort + BM_E_COMM when the communicator is already aborted or
+// RCCL reports an asynchronous error (a peer that died, a transport failure).
+int comm_health(Comm *c, const char *who) {
+  if (c->aborted) {
+    bm_set_error("%s: communicator aborted earlier: %s", who, c->why);
+    return BM_E_COMM;
+  }
+  ncclResult_t async = ncclSuccess;
+  const ncclResult_t r = g_rccl.commGetAsyncError(c->comm, &async);
+  if (r != ncclSuccess || (async != ncclSuccess && async != ncclInProgress)) {
+    char why[200];
+    std::snprintf(why, sizeof(why), "RCCL asynchronous error: %s",
+                  g_rccl.errorString(r != ncclSuccess ? r : async));
+    return comm_fail(c, who, why);
+  }
+  return BM_OK;
+}
 
 }  // namespace
 
@@ -166,7 +201,7 @@ extern "C" int bm_comm_destroy(void *comm) {
   if (!comm) return BM_OK;
   Comm *c = static_cast<Comm *>(comm);
   int rc = BM_OK;
-  if (rccl("bm_comm_destroy") == BM_OK)
+  if (!c->aborted && rccl("bm_comm_destroy") == BM_OK)  // (an aborted handle is already released)
     rc = nccl_check(g_rccl.commDestroy(c->comm), "bm_comm_destroy", "ncclCommDestroy");
   delete c;
   return rc;
@@ -186,8 +221,9 @@ extern "C" int bm_comm_info(void *comm, int *rank, int *world, char *lib, size_t
 
 // Variable-size all-to-all of byte blocks: block q of `send` (send_bytes[q]
 // at send_offs[q]) goes to rank q; block s of `recv` (recv_bytes[s] at
-// recv_offs[s]) comes from rank s.  One RCCL group of point-to-point pairs
-// (the self block included), stream-ordered on `stream`.
+// recv_offs[s]) comes from rank s.  The self block is a local device copy on
+// `stream`; the peers are one RCCL group of point-to-point pairs, all
+// stream-ordered on `stream`.
 extern "C" int bm_alltoallv(void *comm, const void *send, const int64_t *send_bytes,
                             const int64_t *send_offs, void *recv, const int64_t *recv_bytes,
                             const int64_t *recv_offs, void *stream) {
@@ -195,7 +231,7 @@ extern "C" int bm_alltoallv(void *comm, const void *send, const int64_t *send_by
     bm_set_error("bm_alltoallv: null argument");
     return BM_E_ARG;
   }
-  const Comm *c = static_cast<const Comm *>(comm);
+  Comm *c = static_cast<Comm *>(comm);
   for (int q = 0; q < c->world; ++q) {
     if (send_bytes[q] < 0 || recv_bytes[q] < 0 || send_offs[q] < 0 || recv_offs[q] < 0 ||
         (send_bytes[q] && !send) || (recv_bytes[q] && !recv)) {
@@ -205,14 +241,31 @@ extern "C" int bm_alltoallv(void *comm, const void *send, const int64_t *send_by
       return BM_E_ARG;
     }
   }
+  const int me = c->rank;
+  if (send_bytes[me] != recv_bytes[me]) {  // the one pairing this rank can check alone
+    bm_set_error("bm_alltoallv: self block mismatch (sends %lld bytes to itself, expects %lld)",
+                 (long long)send_bytes[me], (long long)recv_bytes[me]);
+    return BM_E_ARG;
+  }
   if (int rc = rccl("bm_alltoallv")) return rc;
+  if (int rc = comm_health(c, "bm_alltoallv")) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (send_bytes[me]) {
+    const hipError_t e = hipMemcpyAsync(static_cast<char *>(recv) + recv_offs[me],
+                                        static_cast<const char *>(send) + send_offs[me], (size_t)send_bytes[me],
+                                        hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) {
+      bm_set_error("bm_alltoallv: self-block copy failed: %s", hipGetErrorString(e));
+      return BM_E_HIP;
+    }
+  }
+  if (c->world == 1) return BM_OK;
   if (int rc = nccl_check(g_rccl.groupStart(), "bm_alltoallv", "ncclGroupStart")) return rc;
   int rc = BM_OK;
-  for (int k = 0; k < c->world && rc == BM_OK; ++k) {
+  for (int k = 1; k < c->world && rc == BM_OK; ++k) {
     // rank r pairs with r+k (send) and r-k (recv): every link busy at once
-    const int to = (c->rank + k) % c->world;
-    const int from = (c->rank - k + c->world) % c->world;
+    const int to = (me + k) % c->world;
+    const int from = (me - k + c->world) % c->world;
     if (send_bytes[to])
       rc = nccl_check(g_rccl.send(static_cast<const char *>(send) + send_offs[to], (size_t)send_bytes[to],
                                   ncclUint8, to, c->comm, st),
@@ -235,7 +288,7 @@ extern "C" int bm_allgatherv(void *comm, const void *send, int64_t send_bytes, v
     bm_set_error("bm_allgatherv: bad arguments");
     return BM_E_ARG;
   }
-  const Comm *c = static_cast<const Comm *>(comm);
+  Comm *c = static_cast<Comm *>(comm);
   if (recv_bytes[c->rank] != send_bytes) {
     bm_set_error("bm_allgatherv: send_bytes %lld != recv_bytes[rank] %lld", (long long)send_bytes,
                  (long long)recv_bytes[c->rank]);
@@ -250,15 +303,25 @@ extern "C" int bm_allgatherv(void *comm, const void *send, int64_t send_bytes, v
     uniform = uniform && recv_bytes[s] == send_bytes && recv_offs[s] == (int64_t)s * send_bytes;
   }
   if (int rc = rccl("bm_allgatherv")) return rc;
+  if (int rc = comm_health(c, "bm_allgatherv")) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (uniform) {
     if (send_bytes == 0) return BM_OK;
     return nccl_check(g_rccl.allGather(send, recv, (size_t)send_bytes, ncclUint8, c->comm, st), "bm_allgatherv",
                       "ncclAllGather");
   }
+  if (send_bytes) {  // own block: a local device copy
+    const hipError_t e = hipMemcpyAsync(static_cast<char *>(recv) + recv_offs[c->rank], send, (size_t)send_bytes,
+                                        hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) {
+      bm_set_error("bm_allgatherv: own-block copy failed: %s", hipGetErrorString(e));
+      return BM_E_HIP;
+    }
+  }
+  if (c->world == 1) return BM_OK;
   if (int rc = nccl_check(g_rccl.groupStart(), "bm_allgatherv", "ncclGroupStart")) return rc;
   int rc = BM_OK;
-  for (int k = 0; k < c->world && rc == BM_OK; ++k) {
+  for (int k = 1; k < c->world && rc == BM_OK; ++k) {
     const int to = (c->rank + k) % c->world;
     const int from = (c->rank - k + c->world) % c->world;
     if (send_bytes)
@@ -270,4 +333,74 @@ extern "C" int bm_allgatherv(void *comm, const void *send, int64_t send_bytes, v
   }
   const int rc_end = nccl_check(g_rccl.groupEnd(), "bm_allgatherv", "ncclGroupEnd");
   return rc != BM_OK ? rc : rc_end;
+}
+
+// Host wait for everything queued on `stream` (the exchanges of this
+// communicator and whatever precedes them), bounded: RCCL's asynchronous
+// error is polled while waiting, and on an error or after timeout_s seconds
+// the communicator is aborted -- its kernels exit, the stream drains -- and
+// BM_E_COMM comes back instead of a hang (a peer that died or posted a
+// mismatched exchange; the Spark shuffle it replaces, chunk.py:251-261,
+// surfaces a lost executor as an exception the same way).
+extern "C" int bm_comm_wait(void *comm, void *stream, double timeout_s) {
+  if (!comm) {
+    bm_set_error("bm_comm_wait: null communicator");
+    return BM_E_ARG;
+  }
+  Comm *c = static_cast<Comm *>(comm);
+  if (int rc = rccl("bm_comm_wait")) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return c->aborted ? comm_health(c, "bm_comm_wait") : BM_OK;
+    if (q != hipErrorNotReady) {
+      bm_set_error("bm_comm_wait: hipStreamQuery: %s", hipGetErrorString(q));
+      return BM_E_HIP;
+    }
+    if (int rc = comm_health(c, "bm_comm_wait")) {
+      // aborted: RCCL's kernels exit; give the stream a bounded time to drain
+      const auto ta = std::chrono::steady_clock::now();
+      while (hipStreamQuery(st) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - ta < std::chrono::seconds(10))
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      return rc;
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s > 0 && el > timeout_s) {
+      char why[200];
+      std::snprintf(why, sizeof(why),
+                    "exchange not complete after %.1f s (a peer rank failed, stalled or posted a mismatched "
+                    "exchange)", el);
+      comm_fail(c, "bm_comm_wait", why);
+      const auto ta = std::chrono::steady_clock::now();
+      while (hipStreamQuery(st) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - ta < std::chrono::seconds(10))
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      return BM_E_COMM;
+    }
+    // spin briefly (exchanges of a few ms), then back off to 200 us polls
+    if (++spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+// Non-blocking health check: BM_OK, or BM_E_COMM (and the communicator
+// aborted) after an asynchronous RCCL error or an earlier abort.
+extern "C" int bm_comm_check(void *comm) {
+  if (!comm) {
+    bm_set_error("bm_comm_check: null communicator");
+    return BM_E_ARG;
+  }
+  if (int rc = rccl("bm_comm_check")) return rc;
+  return comm_health(static_cast<Comm *>(comm), "bm_comm_check");
+}
+
+// Abort a communicator now (ncclCommAbort): pending exchanges stop, every
+// later call on it returns BM_E_COMM.  bm_comm_destroy still frees the handle.
+extern "C" int bm_comm_abort(void *comm) {
+  if (!comm) return BM_OK;
+  if (int rc = rccl("bm_comm_abort")) return rc;
+  comm_fail(static_cast<Comm *>(comm), "bm_comm_abort", "aborted by the caller");
+  return BM_OK;
 }

@@ -759,17 +759,29 @@ __device__ __forceinline__ uint64_t sq32(int32_t x) {
   return (uint64_t)(a * a);
 }
 
-// (n, S1, S2) -> (mean, M2) with the n S2 - S1^2 difference in 128 bits
-__device__ __forceinline__ void int_moments(uint64_t n, int64_t s1, uint64_t s2, double &mean, double &m2) {
+// (n, S1, S2) -> (mean, M2) with the n S2 - S1^2 difference in 128 bits.  S2
+// arrives as a 128-bit (hi, lo) pair: one chunk's S2 fits 64 bits (the host
+// caps a chunk at 2^31 rows, x^2 < 2^32), but the sum over chunks does not
+// once an output covers 2^32 values of magnitude ~2^16 (an 8 GiB uint16
+// var(axis=None)).  n < 2^38 and S2 < 2^70, so n S2 < 2^108; |S1| < 2^54.
+__device__ __forceinline__ void int_moments(uint64_t n, int64_t s1, uint64_t s2, uint64_t s2_hi, double &mean,
+                                            double &m2) {
   mean = n ? (double)s1 / (double)n : 0.0;
   const uint64_t a1 = (uint64_t)(s1 < 0 ? -s1 : s1);
   // n * s2 and a1 * a1 as (hi, lo)
-  const uint64_t p_lo = n * s2, p_hi = __umul64hi(n, s2);
+  const uint64_t p_lo = n * s2, p_hi = __umul64hi(n, s2) + n * s2_hi;
   const uint64_t q_lo = a1 * a1, q_hi = __umul64hi(a1, a1);
   const uint64_t lo = p_lo - q_lo;
   const uint64_t hi = p_hi - q_hi - (p_lo < q_lo ? 1 : 0);
   const double num = (double)hi * 18446744073709551616.0 + (double)lo;  // >= 0 (Cauchy-Schwarz)
   m2 = n ? num / (double)n : 0.0;
+}
+
+// 128-bit running S2: (hi, lo) += v
+__device__ __forceinline__ void add128(uint64_t &lo, uint64_t &hi, uint64_t v_lo, uint64_t v_hi) {
+  const uint64_t t = lo + v_lo;
+  hi += v_hi + (t < lo ? 1 : 0);
+  lo = t;
 }
 
 // chunk partials (workspace) stay exact integer sums, merged by the combine
@@ -782,7 +794,7 @@ __device__ __forceinline__ void emit_int_mom(const Sink &sk, int64_t idx, int64_
     return;
   }
   double mean, m2;
-  int_moments((uint64_t)n, s1, s2, mean, m2);
+  int_moments((uint64_t)n, s1, s2, 0, mean, m2);
   emit_mom(sk, idx, e, c, (double)n, mean, m2, 0.0);
 }
 
@@ -943,17 +955,17 @@ __global__ void __launch_bounds__(kThreads)
     if constexpr (MODE == M_MOM) {
       if (d.int_sums) {  // exact: add the chunks' integer sums
         int64_t s1 = 0, cnt = 0;
-        uint64_t s2 = 0;
+        uint64_t s2 = 0, s2_hi = 0;
         for (int64_t p = 0; p < d.nparts; ++p) {
           const int64_t nb = min(d.R, (p + 1) * d.rchunk) - p * d.rchunk;
           if (nb <= 0) continue;
           const int64_t at = p * d.part_stride + e;
           s1 += reinterpret_cast<const int64_t *>(p0)[at];
-          s2 += reinterpret_cast<const uint64_t *>(p1)[at];
+          add128(s2, s2_hi, reinterpret_cast<const uint64_t *>(p1)[at], 0);
           cnt += nb;
         }
         double mean, m2;
-        int_moments((uint64_t)cnt, s1, s2, mean, m2);
+        int_moments((uint64_t)cnt, s1, s2, s2_hi, mean, m2);
         emit_mom(sk, e, e, 1, (double)cnt, mean, m2, 0.0);
         continue;
       }
@@ -994,7 +1006,7 @@ struct PartState {
   double n, m, q;
   uint64_t u;
   int64_t s1, cnt;
-  uint64_t s2;
+  uint64_t s2, s2_hi;  // 128-bit sum of the chunks' S2
   int any;
 };
 
@@ -1006,7 +1018,8 @@ __device__ __forceinline__ void merge_state(PartState &a, const PartState &b, bo
     return;
   }
   if (MODE == M_MOM && int_sums) {
-    a.s1 += b.s1; a.s2 += b.s2; a.cnt += b.cnt;
+    a.s1 += b.s1; a.cnt += b.cnt;
+    add128(a.s2, a.s2_hi, b.s2, b.s2_hi);
   } else if (MODE == M_MEAN || MODE == M_MOM) {
     chan(a.n, a.m, a.q, b.n, b.m, b.q, MODE == M_MOM);
   } else if (facc_mode<MODE>()) {
@@ -1062,7 +1075,7 @@ __global__ void __launch_bounds__(kThreads)
   if constexpr (MODE == M_MOM) {
     if (int_sums) {
       double mean, m2;
-      int_moments((uint64_t)r.cnt, r.s1, r.s2, mean, m2);
+      int_moments((uint64_t)r.cnt, r.s1, r.s2, r.s2_hi, mean, m2);
       emit_mom(sk, e, e, 1, (double)r.cnt, mean, m2, 0.0);
       return;
     }
@@ -1143,6 +1156,9 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
       const int64_t maxch = std::max<int64_t>(1, R / (64 * vec * 4));
       nch = std::min(nch, maxch);
     }
+    // one chunk's exact integer S2 (x^2 < 2^32 per value) must fit 64 bits:
+    // at most 2^31 values per chunk (a no-op below 4 GiB per output row)
+    nch = std::max<int64_t>(nch, cdiv(R, (int64_t)1 << 31));
     int64_t rc = cdiv(R, nch);
     rc = cdiv(rc, vec) * vec;
     p.rchunk = rc;
@@ -1167,6 +1183,7 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
       nch = std::min(nch, maxch);
     }
     nch = std::min<int64_t>(nch, 65535);
+    nch = std::max<int64_t>(nch, cdiv(R, (int64_t)1 << 31));  // exact integer S2 per chunk < 2^63
     p.rchunk = cdiv(R, nch);
     p.nchunks = cdiv(R, p.rchunk);
   }

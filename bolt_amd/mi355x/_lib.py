@@ -53,14 +53,24 @@ SIGNATURES = {
                                 _c.c_void_p]),
     "bm_allgatherv": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_void_p, _i64p, _i64p,
                                  _c.c_void_p]),
+    "bm_comm_wait": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_double]),
+    "bm_comm_check": (_c.c_int, [_c.c_void_p]),
+    "bm_comm_abort": (_c.c_int, [_c.c_void_p]),
 }
 COMM_ID_BYTES = 128  # BM_COMM_ID_BYTES
+BM_OK, BM_E_ARG, BM_E_HIP, BM_E_WS, BM_E_COMM = 0, -1, -2, -3, -4
 
 _LIB = None
 
 
 class BoltDeviceError(RuntimeError):
     """A libbolt_mi355x call returned an error status."""
+
+
+class BoltCommError(BoltDeviceError):
+    """The RCCL communicator failed (asynchronous error, timeout, abort): a
+    peer rank died, stalled or posted a mismatched exchange.  The communicator
+    is aborted; the arrays of its context cannot exchange records any more."""
 
 
 def load(path=LIB_PATH):
@@ -87,7 +97,8 @@ def load(path=LIB_PATH):
 def check(rc, what):
     if rc != 0:
         msg = _LIB.bm_last_error().decode("utf-8", "replace") if _LIB is not None else ""
-        raise BoltDeviceError("%s failed (%d): %s" % (what, rc, msg))
+        err = BoltCommError if rc == BM_E_COMM else BoltDeviceError
+        raise err("%s failed (%d): %s" % (what, rc, msg))
 
 
 def i64_array(vals):

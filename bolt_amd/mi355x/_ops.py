@@ -87,9 +87,11 @@ def raw_stream(device):
 
 
 class HipBackend(object):
-    """Launches libbolt_mi355x kernels on torch's current stream."""
+    """Launches libbolt_mi355x kernels on torch's current stream.  Between GPUs
+    its records move over the library's own RCCL communicator only."""
 
     name = "hip"
+    transport = "rccl"
 
     def __init__(self):
         self.lib = _lib.load()
@@ -213,7 +215,10 @@ _BACKENDS = {}
 
 
 def register_backend(device_type, backend):
-    """Install a backend for a torch device type (tests only: 'cpu')."""
+    """Install a backend for a torch device type (test executors only: the numpy
+    executor on 'cpu', the host-staged one-GPU rehearsal on 'cuda').  A
+    backend's ``transport`` attribute names how its contexts exchange records
+    across ranks ("rccl", or "torch" / "host" for test executors)."""
     if backend is None:
         _BACKENDS.pop(device_type, None)
     else:

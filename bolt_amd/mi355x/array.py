@@ -417,20 +417,44 @@ class BoltArrayMI355X(BoltArray):
         return self._like(out, self._shape, self._split, dtype=dtype)
 
     def clip(self, min=None, max=None):
-        """Clip values below ``min`` / above ``max`` (array.py:932-945), on the device."""
+        """Clip values below ``min`` / above ``max`` (array.py:932-945), on the device.
+
+        The result dtype is numpy's for ``record.clip(min, max)`` (numpy is asked
+        on a 1-element record, so its errors are numpy's too): a float bound on an
+        integer array promotes.  torch has no max/min kernels for uint16/32/64,
+        so unsigned records are compared in a wider signed type (uint64: with
+        the sign bit flipped, which maps unsigned order onto signed order)."""
         import torch
         from bolt_amd.mi355x import functional as F
-        src = F.view(self._data, self._local_shape, self._dtype)
-        out = src.clone()
+        rdt = np.zeros(1, self._dtype).clip(min=min, max=max).dtype
+        x = F.view(self._data, self._local_shape, self._dtype)
         vs = tuple(self._shape[self._split:])
+        wide = {1: torch.int16, 2: torch.int32, 4: torch.int64}
+        if rdt != self._dtype:
+            x = x.to(F.torch_dtype(rdt))
+        if rdt.kind == "u" and rdt.itemsize < 8:
+            out, back = x.to(wide[rdt.itemsize]), F.torch_dtype(rdt)
+        elif rdt.kind == "u":
+            flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=x.device)
+            out, back = x.view(torch.int64) ^ flip, None
+        else:
+            out, back = x.clone(), None
         for bound, fn in ((min, torch.maximum), (max, torch.minimum)):
             if bound is None:
                 continue
-            b = torch.as_tensor(np.asarray(bound, dtype=self._dtype), device=out.device)
-            if b.ndim > len(vs):
-                raise ValueError("clip bound of shape %s does not broadcast to records %s" % (b.shape, vs))
+            nb = np.asarray(bound).astype(rdt)
+            if nb.ndim > len(vs):
+                raise ValueError("clip bound of shape %s does not broadcast to records %s" % (nb.shape, vs))
+            if rdt.kind == "u" and rdt.itemsize < 8:
+                b = torch.as_tensor(nb.astype(np.int64), device=out.device).to(out.dtype)
+            elif rdt.kind == "u":
+                b = torch.as_tensor(nb.view(np.int64), device=out.device) ^ flip
+            else:
+                b = torch.as_tensor(nb, device=out.device)
             out = fn(out, b)
-        return self._like(F.as_bytes(out), self._shape, self._split)
+        if rdt.kind == "u":
+            out = out.to(back) if back is not None else (out ^ flip).view(torch.uint64)
+        return self._like(F.as_bytes(out.contiguous()), self._shape, self._split, dtype=rdt)
 
     def repartition(self, npartitions):
         """Records stay sharded one slab per GPU; only the partition count the
@@ -833,9 +857,23 @@ class BoltArrayMI355X(BoltArray):
         ctx = self._ctx
         axset = sorted(set(int(a) for a in axis))
         kept = [i for i in range(self.ndim) if i not in axset]
+        gshape = self._shape
         lshape = self._local_shape
-        perm, O, R, I = reduce_layout(lshape, axset)
         src = self._data
+        if ctx.world_size > 1 and 0 not in axset:
+            # a rank's slab of the sharded axis is a slab of every record: a
+            # function that is not elementwise must see whole records, as the
+            # reference's treeReduce after _align does (array.py:268-269).  Bring
+            # the reduced axes to the front across GPUs (one exchange), so each
+            # rank holds whole records, and reduce the sharded axis below.
+            gperm = axset + kept
+            src = permute_sharded(ctx, self._backend, src, gshape, gperm, self._dtype.itemsize)
+            gshape = tuple(gshape[p] for p in gperm)
+            lo, hi = ctx.local_bounds(gshape[0])
+            lshape = (hi - lo,) + gshape[1:]
+            axset = list(range(len(axset)))
+            kept = list(range(len(axset), len(gshape)))
+        perm, O, R, I = reduce_layout(lshape, axset)
         if perm is not None:
             tmp = _empty(src.numel(), src.device)
             if src.numel():
@@ -853,19 +891,12 @@ class BoltArrayMI355X(BoltArray):
         if ctx.world_size == 1:
             return part.cpu().numpy().astype(out_dtype, copy=False)
         from bolt_amd.mi355x.functional import as_bytes
-        if 0 not in axset:
-            # every rank reduced its own slab of outputs: gather them in rank order
-            out_shape = tuple(self._shape[i] for i in kept)
-            sizes = [int(np.prod((hi - lo,) + out_shape[1:], dtype=np.int64)) * out_dtype.itemsize
-                     for lo, hi in ctx.bounds(self._shape[0])]
-            got = all_gather_bytes(ctx, as_bytes(part.to(recs.device)), sizes)
-            return to_host(got, out_dtype, out_shape)
         # the sharded axis is reduced: rank partials, then the same tree over
         # the ranks that hold records, in rank order
         pbytes = as_bytes(part)
         allp = all_gather_bytes(ctx, pbytes, [pbytes.numel()] * ctx.world_size)
         per = view(allp, (ctx.world_size,) + tuple(part.shape), out_dtype)
-        has = [r for r, (lo, hi) in enumerate(ctx.bounds(self._shape[0])) if hi > lo]
+        has = [r for r, (lo, hi) in enumerate(ctx.bounds(gshape[0])) if hi > lo]
         res = _tree(func, per[has])
         return res.cpu().numpy().astype(numpy_dtype(res.dtype), copy=False)
 

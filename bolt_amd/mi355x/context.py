@@ -5,11 +5,21 @@ Plays the role SparkContext plays for the spark mode
 process drives one GPU; with torch.distributed initialised the records of
 every array are sharded over the ranks along the leading key axis, in
 contiguous slabs as numpy.array_split would cut them (the analogue of
-parallelize's contiguous partitions).  Over an nccl process group the
-context opens its own RCCL communicator in libbolt_mi355x (bm_comm_init; the
-id travels through the group's rendezvous store) and every record exchange
-goes through it; torch.distributed is used for rendezvous and host-side
-metadata only.
+parallelize's contiguous partitions).
+
+Transport between ranks (``transport``) is chosen by the kernel backend, not
+by the process group.  The production HIP backend uses "rccl": the context
+opens its own RCCL communicator in libbolt_mi355x (bm_comm_init; the id
+travels through the group's rendezvous store) and every device byte between
+GPUs goes through it; torch.distributed carries the rendezvous and host-side
+metadata only.  The group must have an nccl device backend ('nccl' or
+'cpu:gloo,cuda:nccl'; with the latter torch never builds an RCCL
+communicator of its own).  Only the test executors registered through
+_ops.register_backend use torch.distributed collectives ("torch", "host").
+
+Every RCCL wait is bounded by ``comm_timeout`` seconds
+(BOLT_AMD_COMM_TIMEOUT, default 600): a peer that dies or posts a mismatched
+exchange raises _lib.BoltCommError and aborts the communicator.
 """
 import os
 
@@ -43,12 +53,21 @@ class MI355XContext(object):
         # (no HIP device / library): the mode has no CPU fallback
         from bolt_amd.mi355x._ops import backend_for
         self.backend = backend_for(self.device)
-        # RCCL communicator of libbolt_mi355x (bm_comm_init) for the record
-        # exchanges when the ranks drive GPUs over an nccl (= RCCL) group
         self.comm = None
         self.comm_stream = None
-        if self.world_size > 1 and self.device.type == "cuda" and dist.get_backend(group) == "nccl":
-            self._init_comm()
+        self.comm_timeout = float(os.environ.get("BOLT_AMD_COMM_TIMEOUT", "600"))
+        self.transport = None
+        if self.world_size > 1:
+            self.transport = getattr(self.backend, "transport", "rccl")
+            if self.transport == "rccl":
+                pg = str(dist.get_backend(group))
+                if "nccl" not in pg:
+                    raise RuntimeError(
+                        "bolt_amd: the mi355x mode moves records between GPUs over RCCL; initialise "
+                        "torch.distributed with backend 'nccl' (or 'cpu:gloo,cuda:nccl'), not %r -- "
+                        "device bytes are never staged through the host" % pg)
+                # RCCL communicator of libbolt_mi355x (bm_comm_init) for the record exchanges
+                self._init_comm()
 
     def _init_comm(self):
         """One RCCL communicator over this context's ranks: rank 0 makes the id,
@@ -85,13 +104,23 @@ class MI355XContext(object):
         return "bolt_amd/rccl_id/%s/%d" % (",".join(map(str, ranks)), n)
 
     def close(self):
-        """Release the RCCL communicator (before the process group is destroyed)."""
+        """Release the RCCL communicator (before the process group is destroyed).
+
+        Waits (bounded, bm_comm_wait) for the exchanges still queued on the
+        communicator's stream and on the current stream first; a failed
+        communicator is released without raising again."""
         if self.comm is not None:
             from bolt_amd.mi355x import _lib
             import torch
-            torch.cuda.synchronize(self.device)
-            _lib.check(_lib.load().bm_comm_destroy(self.comm), "bm_comm_destroy")
-            self.comm = None
+            lib = _lib.load()
+            comm, self.comm = self.comm, None
+            try:
+                for st in (self.comm_stream, torch.cuda.current_stream(self.device)):
+                    _lib.check(lib.bm_comm_wait(comm, st.cuda_stream, self.comm_timeout), "bm_comm_wait")
+            except _lib.BoltCommError:
+                pass  # already aborted: destroy only frees the handle
+            finally:
+                _lib.check(lib.bm_comm_destroy(comm), "bm_comm_destroy")
 
     @classmethod
     def default(cls):

@@ -6,14 +6,24 @@ in unchunk, array.py:1012-1014 collect).  Here records are slabs of the
 leading key axis, one slab per rank, and the only exchange a swap needs is
 ONE all-to-all over RCCL (xGMI peer links), issued by libbolt_mi355x itself
 (bm_alltoallv / bm_allgatherv on the context's communicator; torch only owns
-the buffers and streams).  Over a gloo process group (the CPU tests and the
-one-GPU multi-rank rehearsal) the same exchanges use torch.distributed:
+the buffers and streams):
 
   pack    local strided copy of the shard into G contiguous send blocks,
           block q = the part of the permuted array that rank q will own;
   a2a     bm_alltoallv with per-peer byte counts (one RCCL group of
-          ncclSend / ncclRecv pairs, every link at once);
+          ncclSend / ncclRecv pairs, every link at once; the self block is a
+          local device copy);
   unpack  local strided copy of each received block into its place.
+
+The transport is the context's (MI355XContext.transport), chosen by the kernel
+backend, never by the process group: the production HIP backend always uses
+the library's RCCL communicator ("rccl").  Only the test executors registered
+through _ops.register_backend select torch.distributed collectives: "torch"
+(the numpy executor on CPU tensors over gloo) and "host" (the one-GPU
+multi-rank rehearsal, device bytes staged through the host over gloo).
+
+Every RCCL exchange ends in a bounded host wait (bm_comm_wait): a peer that
+died or posted a mismatched exchange raises BoltCommError instead of hanging.
 
 A permutation that keeps the leading axis (perm[0] == 0) needs no exchange.
 Statistics exchange only small per-output states (all_gather), see array.py.
@@ -31,10 +41,34 @@ def _empty(nbytes, device):
 from bolt_amd.mi355x.transfer import to_host  # noqa: E402,F401  (re-exported)
 
 
-# Pipeline depth of the swap exchange (None: from the message size, >= 32 MiB
-# per peer per stage, at most 8 stages); tests set it to exercise the stages.
+# Pipeline depth of the swap exchange: K = per-peer bytes // stage_bytes(G),
+# clamped to [1, 8] (STAGES overrides; tests set it to exercise the stages).
+# Stage i's exchange overlaps stage i-1's unpack and stage i+1's pack; the
+# first pack and the last unpack do not overlap, so deeper is better (each is
+# 1/K of the local work) until a stage's per-peer message gets too small for
+# RCCL to keep a link at its plateau.  The local work moves 2x a stage's bytes
+# through HBM at ~5.8 TB/s (profiles/r01_exchange_local.log) while the links
+# move them at (G-1)*153 GB/s per rank, so at every G the exchange, not the
+# pack/unpack, is the critical path.  The floor per world size is the
+# smallest per-peer message that keeps K = 8 at the BASELINE sizes while
+# staying >= 8 MiB per peer (a send/recv pair is near its plateau from a few
+# MiB); larger worlds split each rank's bytes over more peers, so the floor
+# shrinks with G:
+#   G = 2: 1 peer,  32 MiB     G = 4: 3 peers, 16 MiB     G = 8: 7 peers, 8 MiB
+# (C2 per rank: 1.05 / 0.52 / 0.26 GB per peer -> K = 8 at every G.)
 STAGES = None
-STAGE_BYTES = 32 << 20  # per-peer bytes of one stage (tests lower it)
+STAGE_BYTES_BY_WORLD = {2: 32 << 20, 4: 16 << 20, 8: 8 << 20}
+STAGE_BYTES = None  # override for every world size (tests lower it)
+
+
+def stage_bytes(world):
+    if STAGE_BYTES is not None:
+        return STAGE_BYTES
+    for g in sorted(STAGE_BYTES_BY_WORLD, reverse=True):
+        if world >= g:
+            return STAGE_BYTES_BY_WORLD[g]
+    return STAGE_BYTES_BY_WORLD[2]
+
 
 # Optional phase timing of the exchange (bench.py sets it to a dict):
 # name -> list of (start, end) torch.cuda.Event pairs on the current stream.
@@ -80,14 +114,6 @@ def _unit(nbytes):
     return u
 
 
-def _host_staged(ctx, t):
-    """gloo cannot run these collectives on GPU tensors: stage them through the
-    host (used to rehearse the multi-rank GPU path on a single device; RCCL,
-    the production transport, moves device memory directly over xGMI)."""
-    import torch.distributed as dist
-    return t.device.type == "cuda" and dist.get_backend(ctx.group) == "gloo"
-
-
 class _Work(object):
     """An exchange running on the context's RCCL stream: wait() orders the
     caller's current stream after it (the host never blocks)."""
@@ -105,7 +131,8 @@ def _offsets(sizes):
 
 
 def _rccl_all_gather(ctx, local, sizes):
-    """bm_allgatherv on the current stream (include/bolt_mi355x.h)."""
+    """bm_allgatherv on the current stream (include/bolt_mi355x.h), then a
+    bounded wait for it (bm_comm_wait)."""
     import torch
     from bolt_amd.mi355x import _lib
     recv = _empty(sum(sizes), local.device)
@@ -114,7 +141,17 @@ def _rccl_all_gather(ctx, local, sizes):
     rp = recv.data_ptr() if recv.numel() else None
     _lib.check(_lib.load().bm_allgatherv(ctx.comm, sp, int(sizes[ctx.rank]), rp, _lib.i64_array(sizes),
                                          _lib.i64_array(_offsets(sizes)), stream), "bm_allgatherv")
+    comm_wait(ctx, stream)
     return recv
+
+
+def comm_wait(ctx, stream):
+    """Host wait for ``stream`` (a raw hipStream_t or a torch Stream) bounded by
+    ctx.comm_timeout; an RCCL error or a timeout aborts the communicator and
+    raises _lib.BoltCommError (bm_comm_wait)."""
+    from bolt_amd.mi355x import _lib
+    raw = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    _lib.check(_lib.load().bm_comm_wait(ctx.comm, raw, float(ctx.comm_timeout)), "bm_comm_wait")
 
 
 def _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op):
@@ -144,6 +181,7 @@ def _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op):
         ev[1].record(stream)
         PROFILE.setdefault("rccl", []).append(ev)
     if not async_op:
+        comm_wait(ctx, stream)
         return recv
     done = torch.cuda.Event()
     done.record(stream)
@@ -152,14 +190,40 @@ def _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op):
 
 def all_gather_bytes(ctx, local, sizes):
     """Concatenate every rank's byte tensor (sizes[r] bytes from rank r) on every rank."""
-    import torch
-    import torch.distributed as dist
     if ctx.world_size == 1:
         return local
-    if ctx.comm is not None:
+    if ctx.transport == "rccl":
         return _rccl_all_gather(ctx, local, sizes)
-    if _host_staged(ctx, local):
-        return all_gather_bytes(ctx, local.cpu(), sizes).to(local.device)
+    return _test_all_gather(ctx, local, sizes)
+
+
+def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1, async_op=False):
+    """Variable-size all-to-all of byte blocks; every size is a multiple of ``unit``.
+
+    With async_op the call returns (recv, work): the exchange runs on the
+    collective's own stream and ``work.wait()`` orders the caller's stream
+    after it (no host block on RCCL)."""
+    if ctx.transport == "rccl":
+        return _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op)
+    return _test_all_to_all(ctx, send, send_sizes, recv_sizes, unit, async_op)
+
+
+# --- test executors only (transport "torch" / "host"; see the module docstring)
+
+def _check_test_transport(ctx, t):
+    if ctx.transport not in ("torch", "host"):
+        raise RuntimeError("bolt_amd: transport %r has no torch.distributed path" % (ctx.transport,))
+    if t.device.type == "cuda" and ctx.transport != "host":
+        raise RuntimeError("bolt_amd: device bytes never take the torch.distributed path "
+                           "(the mi355x mode exchanges them over RCCL)")
+
+
+def _test_all_gather(ctx, local, sizes):
+    import torch
+    import torch.distributed as dist
+    _check_test_transport(ctx, local)
+    if ctx.transport == "host" and local.device.type == "cuda":
+        return _test_all_gather(ctx, local.cpu(), sizes).to(local.device)
     m = max(sizes) if sizes else 0
     m = (m + 7) // 8 * 8
     buf = _empty(m, local.device)
@@ -172,17 +236,11 @@ def all_gather_bytes(ctx, local, sizes):
     return torch.cat([o[:s] for o, s in zip(outs, sizes)]) if m else _empty(0, local.device)
 
 
-def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1, async_op=False):
-    """Variable-size all-to-all of byte blocks; every size is a multiple of ``unit``.
-
-    With async_op the call returns (recv, work): the exchange runs on the
-    collective's own stream and ``work.wait()`` orders the caller's stream
-    after it (no host block on RCCL)."""
+def _test_all_to_all(ctx, send, send_sizes, recv_sizes, unit, async_op):
     import torch.distributed as dist
-    if ctx.comm is not None:
-        return _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op)
-    if _host_staged(ctx, send):
-        recv = all_to_all_bytes(ctx, send.cpu(), send_sizes, recv_sizes, unit).to(send.device)
+    _check_test_transport(ctx, send)
+    if ctx.transport == "host" and send.device.type == "cuda":
+        recv = _test_all_to_all(ctx, send.cpu(), send_sizes, recv_sizes, unit, False).to(send.device)
         return (recv, None) if async_op else recv
     recv = _empty(sum(recv_sizes), send.device)
     ws, ss = _wide(send, send_sizes, unit)
@@ -236,7 +294,7 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
     # from global quantities only: the largest slab's per-peer block
     max_rows = max(hi_ - lo_ for lo_, hi_ in in_b)
     per_peer = max_rows * int(np.prod(shape[1:])) * es // G
-    K = STAGES if STAGES else int(max(1, min(8, per_peer // STAGE_BYTES)))
+    K = STAGES if STAGES else int(max(1, min(8, per_peer // stage_bytes(G))))
     K = max(1, min(K, min(b - a_ for a_, b in out_b) or 1))
 
     def sub(q, k):
@@ -289,6 +347,10 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
                 _unpack(backend, pending, out, tstr, j, es, even_in)
             pending = (recv, work, send, rparts, recv_sizes, mlo - lo)
         _unpack(backend, pending, out, tstr, j, es, even_in)
+        if ctx.transport == "rccl":
+            # bounded host wait for the last exchange (the final unpack is
+            # already queued behind it): a failed peer raises, never hangs
+            comm_wait(ctx, ctx.comm_stream)
     return out
 
 

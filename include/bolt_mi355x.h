@@ -37,6 +37,7 @@ extern "C" {
 #define BM_E_ARG (-1)    /* invalid argument (shape, stride, dtype, ...)   */
 #define BM_E_HIP (-2)    /* a HIP runtime call failed (launch, ...)       */
 #define BM_E_WS (-3)     /* workspace too small                            */
+#define BM_E_COMM (-4)   /* communicator failed: async RCCL error, timeout or abort */
 
 /* element dtypes understood by the reductions (numpy kinds) */
 #define BM_BOOL 0
@@ -249,10 +250,13 @@ int bm_comm_info(void *comm, int *rank, int *world, char *lib, size_t lib_bytes)
 /*
  * bm_alltoallv -- block q of send (send_bytes[q] bytes at send_offs[q]) goes
  * to rank q; block s of recv (recv_bytes[s] at recv_offs[s]) arrives from rank
- * s.  One RCCL group of ncclSend / ncclRecv pairs, every peer at once (each
- * ordered GPU pair has its own xGMI link), the self block included.  The
- * multi-GPU swap's exchange step (pack -> bm_alltoallv -> unpack).  Arrays
- * have `world` entries; send_bytes[q] must equal what rank q expects.
+ * s.  The self block is a local device copy on `stream` (send_bytes[rank]
+ * must equal recv_bytes[rank], else BM_E_ARG); the peers are one RCCL group of
+ * ncclSend / ncclRecv pairs, every peer at once (each ordered GPU pair has its
+ * own xGMI link).  The multi-GPU swap's exchange step (pack -> bm_alltoallv ->
+ * unpack).  Arrays have `world` entries; send_bytes[q] must equal what rank q
+ * expects (a mismatch across ranks is caught by bm_comm_wait's timeout).
+ * BM_E_COMM if the communicator has failed or been aborted.
  */
 int bm_alltoallv(void *comm, const void *send, const int64_t *send_bytes,
                  const int64_t *send_offs, void *recv, const int64_t *recv_bytes,
@@ -267,6 +271,25 @@ int bm_alltoallv(void *comm, const void *send, const int64_t *send_bytes,
  */
 int bm_allgatherv(void *comm, const void *send, int64_t send_bytes, void *recv,
                   const int64_t *recv_bytes, const int64_t *recv_offs, void *stream);
+
+/*
+ * bm_comm_wait -- block the host until all work queued on `stream` is done,
+ * polling RCCL's asynchronous error meanwhile.  On an RCCL error, or when the
+ * work is not done after timeout_s seconds (<= 0: no limit), the communicator
+ * is aborted (ncclCommAbort: its kernels exit and the stream drains) and
+ * BM_E_COMM is returned with the reason in bm_last_error() -- a lost or
+ * mismatched peer becomes an error, not a hang.  This is how a failed Spark
+ * shuffle (chunk.py:251-261) surfaces: as an exception on the driver.
+ */
+int bm_comm_wait(void *comm, void *stream, double timeout_s);
+
+/* Non-blocking: BM_OK, or BM_E_COMM (communicator aborted) after an
+ * asynchronous RCCL error or an earlier abort. */
+int bm_comm_check(void *comm);
+
+/* Abort now: pending exchanges stop, later calls return BM_E_COMM.
+ * bm_comm_destroy still releases the handle. */
+int bm_comm_abort(void *comm);
 
 #ifdef __cplusplus
 }

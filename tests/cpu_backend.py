@@ -43,6 +43,7 @@ def _unbits64(u, dt):
 
 class CpuBackend(object):
     name = "cpu-test"
+    transport = "torch"  # torch.distributed collectives on CPU tensors (gloo)
 
     def copy_strided(self, src, src_off, dst, dst_off, shape, sstrides, dstrides, es):
         if len(shape) == 0:
@@ -209,6 +210,19 @@ class CpuBackend(object):
 def install():
     from bolt_amd.mi355x._ops import register_backend
     register_backend("cpu", CpuBackend())
+
+
+def install_host_staged_gpu():
+    """The one-GPU multi-rank rehearsal: the HIP kernels, with the records
+    exchanged over a gloo group through the host (RCCL refuses two ranks on one
+    GPU).  A test executor only -- production contexts exchange over RCCL."""
+    from bolt_amd.mi355x._ops import HipBackend, register_backend
+
+    class HostStagedHip(HipBackend):
+        name = "hip-host-staged-rehearsal"
+        transport = "host"
+
+    register_backend("cuda", HostStagedHip())
 
 
 def uninstall():

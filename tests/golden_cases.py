@@ -70,13 +70,15 @@ def truth_stat(x, name, axis):
 
 
 def stat_close(got, ref, truth, out_dtype, x, name="mean"):
-    """The parity rule of SURVEY.md 8(c): |got-ref| <= rtol*|ref| + rtol*scale, with
-    rtol 1e-6 (float32/float16 outputs) / 1e-12 (float64).  The scale has the units
-    of the statistic: max|x| for mean and sum, the reference's own variance
-    magnitude for var (its square root for std) -- never max|x| for var/std, which
-    would relax the bar on offset data.  A result that is at least as close to the
-    float128 truth as the reference's also passes (the reference accumulates
-    float32 statistics in float32, order-dependently)."""
+    """The parity rule of SURVEY.md 8(c): |got-ref| <= rtol*|ref| + atol, with
+    rtol 1e-6 (float32/float16 outputs) / 1e-12 (float64).  For mean and sum
+    atol = rtol*max|x| (the statistic's units).  For var / std the bar is the
+    pure relative one, rtol*|ref|, plus only an eps-sized floor
+    atol = rtol*eps*max|ref| so that a zero variance may come out as a tiny
+    positive one -- never max|x| (which would relax the bar on offset data) and
+    never a second rtol*|ref| (which would double it).  A result that is at
+    least as close to the float128 truth as the reference's also passes (the
+    reference accumulates float32 statistics in float32, order-dependently)."""
     got = np.asarray(got, dtype=np.longdouble)
     ref = np.asarray(ref, dtype=np.longdouble)
     truth = np.asarray(truth, dtype=np.longdouble).reshape(ref.shape)
@@ -85,8 +87,8 @@ def stat_close(got, ref, truth, out_dtype, x, name="mean"):
         rtol = 1e-3
     finite = np.abs(ref[np.isfinite(ref)]) if ref.size else ref
     if name in ("var", "std", "variance", "stdev"):
-        # per output: its own magnitude; a zero variance must come out (near) zero
-        scale = np.abs(ref) + np.finfo(out_dtype).eps * (float(np.max(finite)) if finite.size else 0.0)
+        # pure relative per output; the eps floor lets a zero variance come out (near) zero
+        scale = np.finfo(out_dtype).eps * (float(np.max(finite)) if finite.size else 0.0)
     else:
         xa = np.abs(np.asarray(x, dtype=np.longdouble))
         xa = xa[np.isfinite(xa)]

@@ -26,9 +26,11 @@ def _worker(rank, world, port, errq, device):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from bolt_amd import MI355XContext
+        import cpu_backend
         if device == "cpu":
-            import cpu_backend
             cpu_backend.install()
+        else:
+            cpu_backend.install_host_staged_gpu()
         ctx = MI355XContext(device=device)
         from test_fuzz_oracle import check_case
         for seed in SEEDS:

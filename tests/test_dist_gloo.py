@@ -35,9 +35,11 @@ def _body(rank, world, device="cpu"):
     sys.path[:0] = [here, os.path.dirname(here)]
     import bolt_amd as bolt
     from bolt_amd import MI355XContext
+    import cpu_backend
     if device == "cpu":
-        import cpu_backend
         cpu_backend.install()
+    else:
+        cpu_backend.install_host_staged_gpu()
     ctx = MI355XContext(device=device)
     assert ctx.world_size == world and ctx.rank == rank
 
@@ -89,7 +91,7 @@ def _body(rank, world, device="cpu"):
         bu = bolt.array(u, ctx)
         assert _exact(bu.swap((0,), (0, 1)).toarray(), u.transpose(1, 2, 0)), shp
         assert _exact(bu.transpose(2, 0, 1).toarray(), u.transpose(2, 0, 1)), shp
-    bdist.STAGE_BYTES = 32 << 20
+    bdist.STAGE_BYTES = None
     assert _exact(ba.keys.transpose((1, 0)).toarray(), a.transpose(1, 0, 2, 3))
     assert _exact(ba.keys.reshape((15,)).toarray(), a.reshape(15, 4, 2))
     assert _exact(ba.values.reshape((8,)).toarray(), a.reshape(5, 3, 8))
@@ -193,6 +195,18 @@ def _body(rank, world, device="cpu"):
         a = np.asarray(got.toarray() if hasattr(got, "toarray") else got)
         assert G.reduce_close(a, G.arr(case, "out"), xg, case["func"], ax), case["id"]
 
+    # a user function that is not elementwise, over a non-leading axis: every
+    # call must see whole records (array.py:268-269 aligns first).
+    # Matrix products of 4x4 records in record order (associative, not
+    # commutative, exact in int64): the tree's bracketing cannot change it.
+    mats = np.random.default_rng(5).integers(0, 2, size=(4, 5, 4)).astype(np.int64)
+    bm = bolt.array(mats, ctx)
+    got = np.asarray(bm.reduce(lambda p, q: p @ q, axis=(1,)).toarray())
+    want = np.linalg.multi_dot([mats[:, k, :] for k in range(5)])
+    assert _exact(got, want), (got, want)
+    got = np.asarray(bm.reduce(lambda p, q: p + q.sum(), axis=(1,)).toarray())
+    assert got.shape == (4, 4) and got.dtype == np.int64
+
     # indexing: every golden getitem / squeeze case (rows move between ranks
     # for selections on the sharded axis; squeezing it re-slabs)
     for case in G.cases("getitem") + G.cases("squeeze"):
@@ -248,6 +262,75 @@ def _run(world, device):
 @pytest.mark.parametrize("world", [2, 3])
 def test_multirank_gloo(world):
     _run(world, "cpu")
+
+
+def _transport_worker(rank, world, port, errq):
+    """Production transport ("rccl", the HIP backend's) over a gloo-only group
+    must refuse -- no host staging of device bytes -- and the test transports
+    must never take device tensors."""
+    import sys
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import cpu_backend
+        from bolt_amd import MI355XContext
+        from bolt_amd.mi355x import dist as bdist
+        from bolt_amd.mi355x._ops import register_backend
+
+        class ProductionLike(cpu_backend.CpuBackend):
+            transport = "rccl"   # what HipBackend declares
+
+        register_backend("cpu", ProductionLike())
+        try:
+            MI355XContext(device="cpu")
+        except RuntimeError as e:
+            assert "RCCL" in str(e) and "gloo" in str(e), str(e)
+        else:
+            raise AssertionError("a gloo group was accepted for the RCCL transport")
+        cpu_backend.install()
+        ctx = MI355XContext(device="cpu")
+        assert ctx.transport == "torch" and ctx.comm is None
+
+        class _Dev(object):
+            type = "cuda"
+
+        class _FakeCuda(object):
+            device = _Dev()
+
+        try:
+            bdist._check_test_transport(ctx, _FakeCuda())
+        except RuntimeError as e:
+            assert "RCCL" in str(e)
+        else:
+            raise AssertionError("device bytes took the torch.distributed path")
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_production_transport_refuses_gloo_group():
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, 2, port, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
+    assert all(p.exitcode == 0 for p in procs)
 
 
 @pytest.mark.gpu

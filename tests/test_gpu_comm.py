@@ -1,10 +1,12 @@
 """The RCCL layer of libbolt_mi355x (include/bolt_mi355x.h, bm_comm.hip) on one GPU.
 
 A world-1 communicator drives every entry point: the id, init, info, the
-all-to-all (self block through an RCCL send/recv pair, sync and on the
-context's RCCL stream with event fences, as the pipelined swap uses it), the
-all-gather in both its ncclAllGather form and its point-to-point form, and
-destroy.  The multi-rank logic around these calls (block sizes, offsets,
+all-to-all (the self block is a local device copy; sync and on the context's
+RCCL stream with event fences, as the pipelined swap uses it), the
+all-gather in both its ncclAllGather form and its point-to-point form, the
+error paths (a mismatched self block is refused; a wait that times out
+aborts the communicator and every later call fails with BM_E_COMM instead of
+hanging), and destroy.  The multi-rank logic around these calls (block sizes, offsets,
 stages) is exercised by tests/test_dist_gloo.py over gloo; RCCL cannot put
 two ranks on one GPU, so N > 1 over RCCL runs in the driver's 8-GPU bench.
 Reference site replaced: bolt/spark/chunk.py:251-261 (shuffle #1).
@@ -43,6 +45,78 @@ class _Ctx(object):
         self.comm = comm
         self.comm_stream = torch.cuda.Stream()
         self.rank, self.world_size = 0, 1
+        self.transport = "rccl"
+        self.comm_timeout = 60.0
+
+
+def _new_comm():
+    lib = _lib.load()
+    uid = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+    _lib.check(lib.bm_comm_unique_id(uid, _lib.COMM_ID_BYTES), "bm_comm_unique_id")
+    c = ctypes.c_void_p()
+    _lib.check(lib.bm_comm_init(ctypes.byref(c), 1, uid, 0), "bm_comm_init")
+    return c.value
+
+
+def test_mismatched_self_block_is_an_error(comm):
+    """send_bytes[rank] != recv_bytes[rank]: refused before anything is queued."""
+    import torch
+    lib = _lib.load()
+    x = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    y = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    rc = lib.bm_alltoallv(comm, x.data_ptr(), _lib.i64_array([4096]), _lib.i64_array([0]), y.data_ptr(),
+                          _lib.i64_array([2048]), _lib.i64_array([0]), torch.cuda.current_stream().cuda_stream)
+    assert rc == _lib.BM_E_ARG
+    assert b"self block mismatch" in lib.bm_last_error()
+    assert lib.bm_comm_check(comm) == 0  # the communicator is unharmed
+
+
+def test_wait_timeout_aborts_instead_of_hanging():
+    """A stream that does not drain within the limit (a spin kernel standing in
+    for an exchange whose peer never posts): bm_comm_wait returns BM_E_COMM,
+    the communicator is aborted, later exchanges fail fast, destroy works."""
+    import time
+    import torch
+    lib = _lib.load()
+    c = _new_comm()
+    st = torch.cuda.Stream()
+    # calibrate torch's spin kernel to ~1 s (bounded: it always ends)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):
+        e0.record()
+        torch.cuda._sleep(10 ** 7)
+        e1.record()
+    torch.cuda.synchronize()
+    per = max(e0.elapsed_time(e1), 1e-3) / 1e7           # ms per cycle
+    cycles = int(min(2e11, 1000.0 / per))
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(cycles)
+    t0 = time.perf_counter()
+    rc = lib.bm_comm_wait(c, st.cuda_stream, 0.1)
+    waited = time.perf_counter() - t0
+    assert rc == _lib.BM_E_COMM, rc
+    assert b"not complete" in lib.bm_last_error()
+    assert waited < 15.0
+    assert lib.bm_comm_check(c) == _lib.BM_E_COMM
+    x = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    rc = lib.bm_alltoallv(c, x.data_ptr(), _lib.i64_array([64]), _lib.i64_array([0]), x.data_ptr(),
+                          _lib.i64_array([64]), _lib.i64_array([0]), st.cuda_stream)
+    assert rc == _lib.BM_E_COMM
+    with pytest.raises(_lib.BoltCommError):
+        _lib.check(rc, "bm_alltoallv")
+    torch.cuda.synchronize()   # the spin kernel ends by itself
+    assert lib.bm_comm_destroy(c) == 0
+
+
+def test_wait_ok_and_abort(comm):
+    import torch
+    lib = _lib.load()
+    st = torch.cuda.current_stream()
+    assert lib.bm_comm_wait(comm, st.cuda_stream, 5.0) == 0
+    c = _new_comm()
+    assert lib.bm_comm_abort(c) == 0
+    assert lib.bm_comm_check(c) == _lib.BM_E_COMM
+    assert lib.bm_comm_destroy(c) == 0
 
 
 def test_info_and_errors(comm):
@@ -105,12 +179,13 @@ sys.path.insert(0, os.environ["BM_ROOT"])
 import numpy as np, torch, torch.distributed as dist
 os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ["BM_PORT"])
 torch.cuda.set_device(0)
-dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+dist.init_process_group("cpu:gloo,cuda:nccl", rank=0, world_size=1)  # as bench.py: no eager torch comm
 from bolt_amd import MI355XContext
 from bolt_amd.mi355x import dist as D
 ctx = MI355XContext(device="cuda:0")
 assert ctx.comm is None          # world 1: no exchange, no communicator
 ctx._init_comm()                 # the rendezvous-store path an N-GPU context takes
+ctx.transport = "rccl"
 assert ctx.comm is not None and ctx.comm_stream is not None
 x = torch.arange(1 << 20, dtype=torch.int32, device="cuda").view(torch.uint8)
 recv, work = D._rccl_all_to_all(ctx, x, [x.numel()], [x.numel()], async_op=True)

@@ -187,25 +187,45 @@ def test_stats_full_size_c2(gpu_ctx):
     assert np.all(np.abs(m - mref) <= 1e-6 * np.abs(mref) + np.spacing(np.float32(np.abs(mref))))
     assert np.all(np.abs(sd - sref) <= 1e-6 * np.abs(sref) + np.spacing(np.float32(np.abs(sref))))
     v = b.var(axis=0)
-    assert np.all(np.abs(v - var.cpu().numpy().reshape(512, 512)) <= 1e-6 * var.cpu().numpy().reshape(512, 512) + 1e-3)
+    vref = var.cpu().numpy().reshape(512, 512)
+    # the var-scaled rule: rtol 1e-6 of the variance itself + the float32 rounding of the result
+    assert v.dtype == np.float32
+    assert np.all(np.abs(v - vref) <= 1e-6 * vref + np.spacing(np.float32(vref)))
     tot = b.sum()
     assert abs(float(tot) - float(x.sum())) <= 1e-6 * abs(float(x.sum()))
 
 
 def test_stats_full_size_c4_var(gpu_ctx):
+    """C4 var(axis=0) and sum(axis=0) on ALL 1,048,576 outputs.  The reference
+    values are exact: S1 = sum x and S2 = sum x^2 in int64 on the device (x < 2^16,
+    n = 10,000: n*S2 and S1^2 < 2^59), var = (n*S2 - S1^2) / n^2 formed in
+    exact integers; the kernel's result (2 ulp of the exact rational) must be
+    within 3 ulp of this reference (its own rounding adds < 1 ulp), far inside
+    the north_star's 1e-12.  sum keeps uint16 (mod 2^16),
+    as the reference's treeReduce(add) in the record dtype does."""
     import torch
     b, raw = _shard(gpu_ctx, (10000, 1024, 1024), np.uint16, 1, 9)
     v = b.var(axis=0)
-    assert v.dtype == np.float64
+    s = np.asarray(b.sum(axis=0)).reshape(-1)
+    assert v.dtype == np.float64 and s.dtype == np.uint16
+    v = v.reshape(-1)
     x = raw.view(torch.int16).reshape(10000, 1024 * 1024)
-    cols = torch.arange(0, 1024 * 1024, 4099, device="cuda")
-    xs = (x[:, cols].to(torch.int32) & 0xFFFF).double()
-    ref = xs.var(0, unbiased=False).cpu().numpy()
-    got = v.reshape(-1)[cols.cpu().numpy()]
-    assert np.allclose(got, ref, rtol=1e-12, atol=0)
-    s = b.sum(axis=0)
-    ref_s = (xs.sum(0).to(torch.int64) & 0xFFFF).cpu().numpy().astype(np.uint16)
-    assert np.array_equal(np.asarray(s).reshape(-1)[cols.cpu().numpy()], ref_s)
+    n = x.shape[0]
+    step = 1 << 16
+    for lo in range(0, x.shape[1], step):
+        xs = x[:, lo:lo + step].to(torch.int64) & 0xFFFF
+        s1 = xs.sum(0)
+        s2 = (xs * xs).sum(0)
+        del xs
+        num = n * s2 - s1 * s1                       # exact: < 2^59
+        # num / n^2 rounded once: split num = q*n^2 + r exactly, then q + r/n^2
+        q, r = torch.div(num, n * n, rounding_mode="floor"), torch.remainder(num, n * n)
+        exact = q.double() + r.double() / float(n * n)
+        got = torch.from_numpy(np.ascontiguousarray(v[lo:lo + step])).to(x.device)
+        ulp = torch.abs(exact) * 2.0 ** -52
+        assert bool(torch.all(torch.abs(got - exact) <= 3 * ulp + 1e-300)), lo
+        want_s = (s1 & 0xFFFF).cpu().numpy().astype(np.uint16)
+        assert np.array_equal(s[lo:lo + step], want_s), lo
 
 
 def test_getitem_full_size_c2(gpu_ctx):

@@ -42,12 +42,13 @@ def test_rows_single_chunk(gpu_ctx, kind):
     else:
         x += 1e6
     b = bolt.array(x, gpu_ctx, axis=(0,))
-    var = b.var(axis=1)
-    std = b.std(axis=1)
-    sel = rng.choice(x.shape[0], 256, replace=False)
-    t = _truth_rows(x[sel])
-    _check(np.asarray(var)[sel], t, 1e-12)
-    _check(np.asarray(std)[sel], np.sqrt(t), 1e-12)
+    var = np.asarray(b.var(axis=1))
+    std = np.asarray(b.std(axis=1))
+    # every row (8192 outputs), truth in float128, in row blocks to bound host memory
+    for lo in range(0, x.shape[0], 1024):
+        t = _truth_rows(x[lo:lo + 1024])
+        _check(var[lo:lo + 1024], t, 1e-12)
+        _check(std[lo:lo + 1024], np.sqrt(t), 1e-12)
 
 
 @pytest.mark.parametrize("kind", ["outlier", "offset"])
@@ -62,9 +63,10 @@ def test_cols_single_chunk(gpu_ctx, kind):
         x += 1e6
     b = bolt.array(x, gpu_ctx, axis=(0,))
     var = np.asarray(b.var(axis=1))
-    sel = rng.choice(x.shape[0], 64, replace=False)
-    t = x[sel].astype(np.longdouble).var(axis=1)
-    _check(var[sel], t, 1e-12)
+    # every column (2048 x 2 outputs) against the float128 truth
+    for lo in range(0, x.shape[0], 256):
+        t = x[lo:lo + 256].astype(np.longdouble).var(axis=1)
+        _check(var[lo:lo + 256], t, 1e-12)
 
 
 @pytest.mark.parametrize("kind", ["outlier", "offset"])
@@ -116,7 +118,30 @@ def test_small_int_var_is_exact(gpu_ctx, dtype, axis):
     n = x.shape[axis]
     s1 = xi.sum(axis=axis)
     s2 = (xi * xi).sum(axis=axis)
-    for k in range(0, v.size, 17):
+    for k in range(v.size):  # every output
         num = int(n) * int(s2.reshape(-1)[k]) - int(s1.reshape(-1)[k]) ** 2
         exact = num / (n * n)   # Python int / int: correctly rounded
         assert abs(v.reshape(-1)[k] - exact) <= 2 * np.spacing(exact) + 1e-300, (k, v.reshape(-1)[k], exact)
+
+
+def test_small_int_var_s2_beyond_64_bits(gpu_ctx):
+    """the exact-integer var adds every chunk's S2 = sum x^2.  An
+    8.6 GB uint16 array of 65535s (one 0) reduced over all axes has
+    S2 = (n-1) 65535^2 ~ 2^64: the sum over chunks must not wrap (128-bit
+    combine).  Exact value from Python integers: var = (n-1) 65535^2 / n^2."""
+    import torch
+    from fractions import Fraction
+    shape = (4097, 1 << 20)
+    n = shape[0] * shape[1]
+    raw = torch.full((n,), -1, dtype=torch.int16, device="cuda")   # 0xFFFF = 65535
+    raw[0] = 0
+    b = bolt.ConstructMI355X.fromshards(raw.view(torch.uint8), shape, context=gpu_ctx, split=1, dtype=np.uint16)
+    s1, s2 = (n - 1) * 65535, (n - 1) * 65535 ** 2
+    assert s2 >= 2 ** 64
+    exact = float(Fraction(n * s2 - s1 * s1, n * n))
+    v = float(b.var())
+    assert abs(v - exact) <= 2 * np.spacing(exact), (v, exact)
+    sd = float(b.std())
+    assert abs(sd - np.sqrt(exact)) <= 2 * np.spacing(np.sqrt(exact)), (sd, np.sqrt(exact))
+    del b, raw
+    torch.cuda.empty_cache()
