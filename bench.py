@@ -312,14 +312,40 @@ def cpu_baseline(cfg, shape, dtype, rows):
     u2 = time.perf_counter()
     xs.std(axis=2)
     u3 = time.perf_counter()
-    return {"value": total / (t3 - t0) / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s: "
-                      "swap((0,),(0,1)) %.2fs + mean(axis=2) %.2fs + std(axis=2) %.2fs"
-                      % (str(sample_shape), t1 - t0, t2 - t1, t3 - t2),
-            "host_cpus": os.cpu_count(),
-            "local_numpy": {"value": round(total / (u3 - u0) / 1e9, 3), "unit": "GB/s", "cores": 1,
-                            "sample": "the reference local mode's numpy calls on the same input: transpose "
-                                      "%.2fs + mean %.2fs + std %.2fs" % (u1 - u0, u2 - u1, u3 - u2)}}
+    out = {"value": total / (t3 - t0) / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s: "
+                     "swap((0,),(0,1)) %.2fs + mean(axis=2) %.2fs + std(axis=2) %.2fs"
+                     % (str(sample_shape), t1 - t0, t2 - t1, t3 - t2),
+           "host_cpus": os.cpu_count(),
+           "local_numpy": {"value": round(total / (u3 - u0) / 1e9, 3), "unit": "GB/s", "cores": 1,
+                           "sample": "the reference local mode's numpy calls on the same input: transpose "
+                                     "%.2fs + mean %.2fs + std %.2fs" % (u1 - u0, u2 - u1, u3 - u2)}}
+    del rs, s, xs
+    out["spark_local8"] = spark_local8_baseline(x[:LOCAL8_ROWS], dtype)
+    return out
+
+
+LOCAL8_ROWS = 1000  # time points of the local[8] analogue's sample (~1 GB)
+
+
+def spark_local8_baseline(x, dtype, workers=8):
+    """The Spark local[8] analogue (oracle/spark_local.py): the oracle's record-level
+    C2 step with Spark's stage structure on 8 host processes -- 8 map tasks, one
+    reduce task per chunk group, and the statistics' single task (their _align
+    shuffle has one group) -- shuffles pickled through the parent."""
+    from oracle import spark_local as SL
+    x = np.ascontiguousarray(x)
+    _, _, t, tasks = SL.c2_step(x, workers=workers)
+    N = x.nbytes
+    out = x.shape[1] * x.shape[2] * 4
+    total = 2 * N + 2 * (N + out)
+    return {"value": round(total / t["total"] / 1e9, 4), "unit": "GB/s", "cores": workers,
+            "kind": "port, local[%d] analogue" % workers, "host_cpus": os.cpu_count(),
+            "sample": "oracle/spark_local.py on float32 %s: stage 1 (%d map tasks: chunk + relabel) %.2fs, "
+                      "stage 2 (%d reduce tasks: rebuild + values_to_keys + unchunk) %.2fs, mean(axis=2) %.2fs "
+                      "+ std(axis=2) %.2fs (one task each: _align's shuffle has a single group, as in the "
+                      "reference)" % (str(x.shape), tasks["stage1"], t["stage1"], tasks["stage2"], t["stage2"],
+                                      t["mean"], t["std"])}
 
 
 def main():

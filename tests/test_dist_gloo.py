@@ -198,14 +198,15 @@ def _body(rank, world, device="cpu"):
     # a user function that is not elementwise, over a non-leading axis: every
     # call must see whole records (array.py:268-269 aligns first).
     # Matrix products of 4x4 records in record order (associative, not
-    # commutative, exact in int64): the tree's bracketing cannot change it.
-    mats = np.random.default_rng(5).integers(0, 2, size=(4, 5, 4)).astype(np.int64)
+    # commutative, exact in float64 for 0/1 entries): the bracketing cannot
+    # change it.
+    mats = np.random.default_rng(5).integers(0, 2, size=(4, 5, 4)).astype(np.float64)
     bm = bolt.array(mats, ctx)
     got = np.asarray(bm.reduce(lambda p, q: p @ q, axis=(1,)).toarray())
     want = np.linalg.multi_dot([mats[:, k, :] for k in range(5)])
     assert _exact(got, want), (got, want)
     got = np.asarray(bm.reduce(lambda p, q: p + q.sum(), axis=(1,)).toarray())
-    assert got.shape == (4, 4) and got.dtype == np.int64
+    assert got.shape == (4, 4) and got.dtype == np.float64
 
     # indexing: every golden getitem / squeeze case (rows move between ranks
     # for selections on the sharded axis; squeezing it re-slabs)
