@@ -84,6 +84,17 @@ constexpr int kThreads = 256;
 #ifndef BM_RC_DIAG
 #define BM_RC_DIAG 65536  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this many bytes (0 = off): C3 +8-9%, 64 GiB target +13-15% (profiles/r02_ab_diag.log)
 #endif
+#ifndef BM_RC_DIAG_GFAST
+// rowcopy Diag16 tile order: 1 = the g-tiles (the next-fastest row dim, e.g.
+// C3's k, whose source step is 128 B) vary fastest between consecutive tiles,
+// 0 = the c-tiles (the fastest row dim, source step >= 64 KiB).  With c
+// fastest, the ~256 tiles resident on the GPU all read the same 16 values of
+// g: the same low address bits on every XCD's L2 (one set group per g, ~500
+// lines wanted per 16-way set: TCC tag stalls) and 16 source pages per tile,
+// 4096 in flight.  With g fastest they cover every g (256 distinct low
+// address patterns) and 16x fewer source pages.
+#define BM_RC_DIAG_GFAST 1
+#endif
 #ifndef BM_TR_SKEW
 #define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
 #endif
@@ -128,6 +139,7 @@ struct Diag16 {
   int pad_;
   FastDiv grp;   // Ng * Nc rows per (outer) group
   FastDiv ntc;   // Nc / 16 tiles along c
+  FastDiv ntg;   // Ng / 16 tiles along g
   uint64_t nc;   // Nc
 };
 
@@ -135,7 +147,14 @@ __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   const uint64_t outer = fd_div(row, t.grp);
   const uint64_t q = row - outer * t.grp.d;
   const uint64_t tile = q >> 8, w = q & 255;
-  const uint64_t gt = fd_div(tile, t.ntc), ct = tile - gt * t.ntc.d;
+  uint64_t gt, ct;
+  if (BM_RC_DIAG_GFAST) {
+    ct = fd_div(tile, t.ntg);
+    gt = tile - ct * t.ntg.d;
+  } else {
+    gt = fd_div(tile, t.ntc);
+    ct = tile - gt * t.ntc.d;
+  }
   const uint64_t j = w >> 4, k = w & 15;
   const uint64_t g = gt * 16 + k, c = ct * 16 + ((k + j) & 15);
   return outer * t.grp.d + g * t.nc + c;
@@ -689,6 +708,7 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
         dg.on = 1;
         dg.grp = make_fastdiv((uint64_t)(f.n * g.n));
         dg.ntc = make_fastdiv((uint64_t)(f.n / 16));
+        dg.ntg = make_fastdiv((uint64_t)(g.n / 16));
         dg.nc = (uint64_t)f.n;
       }
     }
