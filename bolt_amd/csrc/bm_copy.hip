@@ -86,14 +86,11 @@ constexpr int kThreads = 256;
 #endif
 #ifndef BM_RC_DIAG_GFAST
 // rowcopy Diag16 tile order: 1 = the g-tiles (the next-fastest row dim, e.g.
-// C3's k, whose source step is 128 B) vary fastest between consecutive tiles,
-// 0 = the c-tiles (the fastest row dim, source step >= 64 KiB).  With c
-// fastest, the ~256 tiles resident on the GPU all read the same 16 values of
-// g: the same low address bits on every XCD's L2 (one set group per g, ~500
-// lines wanted per 16-way set: TCC tag stalls) and 16 source pages per tile,
-// 4096 in flight.  With g fastest they cover every g (256 distinct low
-// address patterns) and 16x fewer source pages.
-#define BM_RC_DIAG_GFAST 1
+// C3's k, 128-B source step) vary fastest between consecutive tiles, so the
+// tiles resident at once read every g instead of the same 16; 0 = the c-tiles
+// (the fastest row dim).  g-fastest measured -6..-11% on the C3 / 64 GiB
+// target swaps (profiles/r03b_ab_diag.log): c-fastest stays.  A/B knob.
+#define BM_RC_DIAG_GFAST 0
 #endif
 #ifndef BM_TR_SKEW
 #define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
@@ -107,6 +104,12 @@ constexpr int kThreads = 256;
 // (round-robin dispatch: block t runs on XCD t % 8, and with 8 b-tiles the
 // b-tile index IS the XCD).  Same tiles per group of blocks, same locality.
 #define BM_TR_ROT 0
+#endif
+#ifndef BM_TR_AFAST
+// transpose: consecutive tiles walk a (the source-contiguous dim) when the
+// source rows of a tile are at least this many bytes apart and a has at least
+// 16 tiles (0 = off, b always fastest: C2 +9% for b, profiles/r01_tv*).  A/B knob.
+#define BM_TR_AFAST 0
 #endif
 #ifndef BM_TR_XCD
 #define BM_TR_XCD 0  // transpose: the blocks one XCD runs take a contiguous eighth of the tiles (A/B knob)
@@ -212,6 +215,9 @@ struct TransDesc {
   FastDiv Lb1, La1;
   int64_t sb2, da2;
   uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (BM_TR_XCD)
+  FastDiv ntA;     // tiles along a
+  int32_t afast;   // consecutive tiles walk a instead of b (BM_TR_AFAST)
+  int32_t pad_;
 };
 
 // TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
@@ -263,8 +269,14 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t t = d.xcd8 ? (t0 % 8) * d.xcd8 + t0 / 8 : t0;
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
-    const uint64_t ta = fd_div(rem, d.ntB);
-    uint64_t tb = rem - ta * d.ntB.d;
+    uint64_t ta, tb;
+    if (d.afast) {
+      tb = fd_div(rem, d.ntA);
+      ta = rem - tb * d.ntA.d;
+    } else {
+      ta = fd_div(rem, d.ntB);
+      tb = rem - ta * d.ntB.d;
+    }
     if (BM_TR_ROT) {
       tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
       if (tb >= d.ntB.d) tb -= d.ntB.d;
@@ -358,8 +370,14 @@ __global__ void __launch_bounds__(NT)
   for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
-    const uint64_t ta = fd_div(rem, d.ntB);
-    uint64_t tb = rem - ta * d.ntB.d;
+    uint64_t ta, tb;
+    if (d.afast) {
+      tb = fd_div(rem, d.ntA);
+      ta = rem - tb * d.ntA.d;
+    } else {
+      ta = fd_div(rem, d.ntB);
+      tb = rem - ta * d.ntB.d;
+    }
     if (BM_TR_ROT) {
       tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
       if (tb >= d.ntB.d) tb -= d.ntB.d;
@@ -948,6 +966,8 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   }
   set_skew(td.batch, batch, es, BM_TR_SKEW);
   td.ntB = make_fastdiv(ntB);
+  td.ntA = make_fastdiv(ntA);
+  td.afast = (BM_TR_AFAST && ntA >= 16 && std::llabs(td.sb) * es >= BM_TR_AFAST) ? 1 : 0;
   td.ntAB = make_fastdiv(ntA * ntB);
   td.ntiles = ntA * ntB * nb;
   td.xcd8 = (BM_TR_XCD && td.ntiles % 8 == 0 && td.ntiles / loop_n <= kMaxGrid && loop_n == 1) ? td.ntiles / 8 : 0;
@@ -968,6 +988,8 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     TransDesc tp = td;
     const uint64_t pA = (uint64_t)((td.La + ta - 1) / ta), pB = (uint64_t)((td.Lb + tbb - 1) / tbb);
     tp.ntB = make_fastdiv(pB);
+    tp.ntA = make_fastdiv(pA);
+    tp.afast = 0;
     tp.ntAB = make_fastdiv(pA * pB);
     tp.ntiles = pA * pB * nb;
     uint64_t g = tp.ntiles / loop_n;

@@ -132,6 +132,16 @@ class RecGather(object):
                                   self.nparts, self.parts, 8, stream())
         assert rc == 0, lib.bm_last_error()
 
+    def check(self):
+        """dst[r, o] == src[r, map[o]] for every record (torch gather, in record blocks)."""
+        s = self.src.view(torch.int64).view(self.nrec, self.src_rec)
+        d = self.dst.view(torch.int64).view(self.nrec, self.dst_rec)
+        idx = self.map.long()
+        for r0 in range(0, self.nrec, 1 << 14):
+            if not torch.equal(s[r0:r0 + (1 << 14)].index_select(1, idx), d[r0:r0 + (1 << 14)]):
+                return False
+        return True
+
 
 class K2V(object):
     """C5's chunked keys_to_values((2,)) as the strided copies chunk.py runs
@@ -177,6 +187,7 @@ OPS = {
     "runs128": lambda: Permute((2048, 2048, 32), (1, 0, 2), np.float32),
     "c3_full": lambda: Permute((4096, 256, 256, 32), (1, 2, 0, 3), np.float32),
     "t64_swap": lambda: Permute((8192, 256, 256, 32), (1, 2, 0, 3), np.float32),
+    "c3T_full": lambda: Permute((4096, 256, 256, 32), (3, 2, 1, 0), np.float32),
     "c4_full": lambda: Permute((10000, 1024, 1024), (1, 0, 2), np.uint16),
     "u16_T": lambda: Permute((2000, 1024, 1024), (2, 1, 0), np.uint16),
     "u8_T": lambda: Permute((2000, 1024, 2048), (2, 1, 0), np.uint8),
