@@ -53,9 +53,6 @@ struct Parts {
 #ifndef BM_STAGE_U
 #define BM_STAGE_U 8
 #endif
-#ifndef BM_RECMAP_PIPE
-#define BM_RECMAP_PIPE 0  // software-pipelined record-map tiles (A/B knob)
-#endif
 #ifndef BM_GATHER_U
 #define BM_GATHER_U 0  // 0: 16 B of map per lane per round
 #endif
@@ -183,138 +180,6 @@ __global__ void __launch_bounds__(kCThreads)
       }
     }
     __syncthreads();
-  }
-}
-
-// Software-pipelined form (BM_RECMAP_PIPE): each block walks its tiles
-// grid-stride and holds the NEXT tile's source in registers (NV 16-B vectors
-// per lane) while it gathers and stores the current one from LDS, so a block
-// keeps loads in flight through its store phase instead of alternating
-// load-wait / store phases.  Tiles: whole-record groups (PARTS = false: rb
-// records per tile) or (record, part) pairs.  16-B staging loads only.
-template <bool PARTS>
-struct TileRange {
-  int64_t s_off, s_n;   // source range (elements)
-  int64_t d_off, d_n;   // destination range (elements)
-  int64_t slo;          // PARTS: source offset of the staged range within the record
-  int64_t dlo;          // PARTS: map offset of the destination range
-};
-
-template <bool PARTS>
-__device__ __forceinline__ TileRange<PARTS> tile_range(int64_t t, const Parts &P, int64_t src_rec, int64_t dst_rec,
-                                                       int64_t nrec, int64_t rb) {
-  TileRange<PARTS> r;
-  if (PARTS) {
-    const int64_t rec = t / P.n;
-    const int p = (int)(t - rec * P.n);
-    r.slo = P.slo[p];
-    r.dlo = P.dlo[p];
-    r.s_off = rec * src_rec + P.slo[p];
-    r.s_n = P.shi[p] - P.slo[p];
-    r.d_off = rec * dst_rec + P.dlo[p];
-    r.d_n = P.dhi[p] - P.dlo[p];
-  } else {
-    const int64_t r0 = t * rb;
-    const int64_t nr = min(rb, nrec - r0);
-    r.slo = 0;
-    r.dlo = 0;
-    r.s_off = r0 * src_rec;
-    r.s_n = nr * src_rec;
-    r.d_off = r0 * dst_rec;
-    r.d_n = nr * dst_rec;
-  }
-  return r;
-}
-
-template <int ES, int VEC, int NV, bool PARTS>
-__global__ void __launch_bounds__(kCThreads)
-    k_recmap_pipe(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ map,
-                  Parts P, int64_t src_rec, int64_t dst_rec, int64_t nrec, int64_t rb, int64_t ntiles,
-                  FastDiv fdst) {
-  typedef typename Elem<ES>::t T;
-  typedef typename VecB<16>::t L;
-  typedef typename VecB<ES * VEC>::t V;
-  constexpr int EPL = 16 / ES;  // elements per staging vector
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const T *lds = reinterpret_cast<const T *>(smem);
-  L *sl = reinterpret_cast<L *>(smem);
-  L reg[NV];
-  int64_t t = blockIdx.x;
-  if (t >= ntiles) return;
-  TileRange<PARTS> cur = tile_range<PARTS>(t, P, src_rec, dst_rec, nrec, rb);
-  {
-    const L *s = reinterpret_cast<const L *>(src + cur.s_off * ES);
-    const int64_t n = cur.s_n / EPL;
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int64_t i = threadIdx.x + (int64_t)u * kCThreads;
-      if (i < n) reg[u] = __builtin_nontemporal_load(s + i);
-    }
-  }
-  for (;;) {
-    {
-      const int64_t n = cur.s_n / EPL;
-#pragma unroll
-      for (int u = 0; u < NV; ++u) {
-        const int64_t i = threadIdx.x + (int64_t)u * kCThreads;
-        if (i < n) sl[i] = reg[u];
-      }
-    }
-    __syncthreads();
-    const int64_t tn = t + gridDim.x;
-    TileRange<PARTS> nxt{};
-    if (tn < ntiles) {  // the next tile's loads fly while this one is gathered and stored
-      nxt = tile_range<PARTS>(tn, P, src_rec, dst_rec, nrec, rb);
-      const L *s = reinterpret_cast<const L *>(src + nxt.s_off * ES);
-      const int64_t n = nxt.s_n / EPL;
-#pragma unroll
-      for (int u = 0; u < NV; ++u) {
-        const int64_t i = threadIdx.x + (int64_t)u * kCThreads;
-        if (i < n) reg[u] = __builtin_nontemporal_load(s + i);
-      }
-    }
-    constexpr int GU = GatherU<VEC>::v;
-    const int64_t nout = cur.d_n / VEC;
-    V *d = reinterpret_cast<V *>(dst + cur.d_off * ES);
-    const int32_t *mp = map + cur.dlo;
-    for (int64_t i0 = threadIdx.x; i0 < nout; i0 += (int64_t)GU * kCThreads) {
-      int32_t m[GU][VEC];
-      int64_t rbase[GU];
-#pragma unroll
-      for (int u = 0; u < GU; ++u) {
-        const int64_t i = i0 + (int64_t)u * kCThreads;
-        if (i < nout) {
-          if (PARTS) {
-            rbase[u] = -cur.slo;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) m[u][k] = mp[i * VEC + k];
-          } else {
-            const uint64_t e = (uint64_t)i * VEC;
-            const uint64_t r = fd_div(e, fdst);
-            const int64_t o = (int64_t)(e - r * fdst.d);
-            rbase[u] = (int64_t)r * src_rec;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) m[u][k] = map[o + k];
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < GU; ++u) {
-        const int64_t i = i0 + (int64_t)u * kCThreads;
-        if (i < nout) {
-          T v[VEC];
-#pragma unroll
-          for (int k = 0; k < VEC; ++k) v[k] = lds[rbase[u] + m[u][k]];
-          V w;
-          __builtin_memcpy(&w, v, sizeof(V));
-          __builtin_nontemporal_store(w, d + i);
-        }
-      }
-    }
-    __syncthreads();
-    if (tn >= ntiles) break;
-    t = tn;
-    cur = nxt;
   }
 }
 
@@ -452,48 +317,6 @@ extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int6
     }
     L.grid = (int)(ntiles < 16384 ? ntiles : 16384);
     const int vec = std::max(1, vb / es);
-    const int64_t nv = ((int64_t)L.shmem + 16 * kCThreads - 1) / (16 * kCThreads);  // staging vectors per lane
-    if (BM_RECMAP_PIPE && lb == 16 && nv <= 16) {
-      // persistent blocks: as many as stay resident (LDS-bound), each walking tiles
-      int per_cu = (int)(160 * 1024 / std::max<size_t>(L.shmem, 1));
-      per_cu = std::max(1, std::min(per_cu, 8));
-      const int64_t cap = (int64_t)256 * per_cu * BM_RECMAP_PIPE;
-      const int grid = (int)std::min<int64_t>(ntiles, cap);
-      const FastDiv fd = make_fastdiv((uint64_t)dst_rec);
-      const int64_t rbv = L.rb;
-#define BM_PIPE_LAUNCH(ESV, VECV, NVV)                                                                         \
-  do {                                                                                                         \
-    if (nparts > 1)                                                                                            \
-      k_recmap_pipe<ESV, VECV, NVV, true><<<grid, kCThreads, L.shmem, st>>>(src, dst, map, P, src_rec, dst_rec, \
-                                                                            nrec, rbv, ntiles, fd);             \
-    else                                                                                                       \
-      k_recmap_pipe<ESV, VECV, NVV, false><<<grid, kCThreads, L.shmem, st>>>(src, dst, map, P, src_rec,        \
-                                                                             dst_rec, nrec, rbv, ntiles, fd);   \
-  } while (0)
-#define BM_PIPE_NV(ESV, VECV)                                       \
-  do {                                                              \
-    if (nv <= 4) BM_PIPE_LAUNCH(ESV, VECV, 4);                      \
-    else if (nv <= 8) BM_PIPE_LAUNCH(ESV, VECV, 8);                 \
-    else BM_PIPE_LAUNCH(ESV, VECV, 16);                             \
-  } while (0)
-      if (es == 8 && vec >= 2) BM_PIPE_NV(8, 2);
-      else if (es == 8) BM_PIPE_NV(8, 1);
-      else if (es == 4 && vec >= 4) BM_PIPE_NV(4, 4);
-      else if (es == 2 && vec >= 8) BM_PIPE_NV(2, 8);
-      else if (es == 1 && vec >= 16) BM_PIPE_NV(1, 16);
-      else goto plain;
-#undef BM_PIPE_NV
-#undef BM_PIPE_LAUNCH
-      {
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) {
-          bm_set_error("bm_record_gather: launch failed: %s", hipGetErrorString(e));
-          return BM_E_HIP;
-        }
-        return BM_OK;
-      }
-    }
-  plain:
     switch (es) {
       case 1: launch_lds<1>(L, lb, vec); break;
       case 2: launch_lds<2>(L, lb, vec); break;

@@ -105,12 +105,6 @@ constexpr int kThreads = 256;
 // b-tile index IS the XCD).  Same tiles per group of blocks, same locality.
 #define BM_TR_ROT 0
 #endif
-#ifndef BM_TR_AFAST
-// transpose: consecutive tiles walk a (the source-contiguous dim) when the
-// source rows of a tile are at least this many bytes apart and a has at least
-// 16 tiles (0 = off, b always fastest: C2 +9% for b, profiles/r01_tv*).  A/B knob.
-#define BM_TR_AFAST 0
-#endif
 #ifndef BM_TR_XCD
 #define BM_TR_XCD 0  // transpose: the blocks one XCD runs take a contiguous eighth of the tiles (A/B knob)
 #endif
@@ -215,9 +209,6 @@ struct TransDesc {
   FastDiv Lb1, La1;
   int64_t sb2, da2;
   uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (BM_TR_XCD)
-  FastDiv ntA;     // tiles along a
-  int32_t afast;   // consecutive tiles walk a instead of b (BM_TR_AFAST)
-  int32_t pad_;
 };
 
 // TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
@@ -269,14 +260,8 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t t = d.xcd8 ? (t0 % 8) * d.xcd8 + t0 / 8 : t0;
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
-    uint64_t ta, tb;
-    if (d.afast) {
-      tb = fd_div(rem, d.ntA);
-      ta = rem - tb * d.ntA.d;
-    } else {
-      ta = fd_div(rem, d.ntB);
-      tb = rem - ta * d.ntB.d;
-    }
+    const uint64_t ta = fd_div(rem, d.ntB);
+    uint64_t tb = rem - ta * d.ntB.d;
     if (BM_TR_ROT) {
       tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
       if (tb >= d.ntB.d) tb -= d.ntB.d;
@@ -370,14 +355,8 @@ __global__ void __launch_bounds__(NT)
   for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
-    uint64_t ta, tb;
-    if (d.afast) {
-      tb = fd_div(rem, d.ntA);
-      ta = rem - tb * d.ntA.d;
-    } else {
-      ta = fd_div(rem, d.ntB);
-      tb = rem - ta * d.ntB.d;
-    }
+    const uint64_t ta = fd_div(rem, d.ntB);
+    uint64_t tb = rem - ta * d.ntB.d;
     if (BM_TR_ROT) {
       tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
       if (tb >= d.ntB.d) tb -= d.ntB.d;
@@ -966,8 +945,6 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   }
   set_skew(td.batch, batch, es, BM_TR_SKEW);
   td.ntB = make_fastdiv(ntB);
-  td.ntA = make_fastdiv(ntA);
-  td.afast = (BM_TR_AFAST && ntA >= 16 && std::llabs(td.sb) * es >= BM_TR_AFAST) ? 1 : 0;
   td.ntAB = make_fastdiv(ntA * ntB);
   td.ntiles = ntA * ntB * nb;
   td.xcd8 = (BM_TR_XCD && td.ntiles % 8 == 0 && td.ntiles / loop_n <= kMaxGrid && loop_n == 1) ? td.ntiles / 8 : 0;
@@ -988,8 +965,6 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     TransDesc tp = td;
     const uint64_t pA = (uint64_t)((td.La + ta - 1) / ta), pB = (uint64_t)((td.Lb + tbb - 1) / tbb);
     tp.ntB = make_fastdiv(pB);
-    tp.ntA = make_fastdiv(pA);
-    tp.afast = 0;
     tp.ntAB = make_fastdiv(pA * pB);
     tp.ntiles = pA * pB * nb;
     uint64_t g = tp.ntiles / loop_n;
