@@ -196,6 +196,45 @@ def steps_of(cfg, b, world=1):
     raise ValueError(cfg)
 
 
+FIRST_OP = {"C1": ((0,), (0,)), "C2": ((0,), (0, 1)), "C3": ((0,), (0,)), "C4": ((0,), (0,)), "C5": "T",
+            "target64": ((0,), (0,))}
+
+
+def exchange_check(torch, cfg, b, ctx, dev, shape=None, dtype=None, split=None):
+    """Bit-exact check of the first op of the step (the swap / .T that crosses
+    GPUs) after the timed region: this rank's slab of the result against the
+    same slab rebuilt from every rank's synthetic shard (regenerated from its
+    seed) and permuted by torch on this GPU.  Returns True if every byte agrees."""
+    from bolt_amd.mi355x.plan import swap_perm
+    if shape is None:
+        shape, dtype, split, _ = CONFIGS[cfg]
+    world = ctx.world_size
+    if FIRST_OP[cfg] == "T":
+        perm, res = list(range(len(shape)))[::-1], b.T
+    else:
+        kax, vax = FIRST_OP[cfg]
+        perm, _ = swap_perm(len(shape), split, kax, vax)
+        res = b.swap(kax, vax)
+    gshape = (shape[0] * world,) + tuple(shape[1:])
+    a = perm[0]
+    idt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[np.dtype(dtype).itemsize]
+    if a == 0:  # no exchange: this rank's own shard
+        want = synth_shard(torch, shape, dtype, dev, 1234 + ctx.rank).permute(*perm).contiguous()
+    else:
+        lo, hi = ctx.bounds(gshape[a])[ctx.rank]
+        parts = []
+        for r in range(world):
+            x = synth_shard(torch, shape, dtype, dev, 1234 + r)
+            parts.append(x.narrow(a, lo, hi - lo).contiguous())
+            del x
+        want = torch.cat(parts, 0).permute(*perm).contiguous()
+        del parts
+    ok = bool(torch.equal(res._data.view(idt), want.view(idt).reshape(-1)))
+    del want, res
+    torch.cuda.empty_cache()
+    return ok
+
+
 # leading-axis rows of the per-GPU shard timed by local_numpy_baseline (~0.5-1 GB)
 LOCAL_SAMPLE_ROWS = {"C3": 64, "C4": 256, "C5": 8, "target64": 64}
 
@@ -469,6 +508,15 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
 
+        check = None
+        if world > 1:
+            # the multi-GPU exchange, bit for bit, outside the timed region
+            ok = exchange_check(torch, cfg, b, ctx, dev)
+            flag = torch.tensor([0.0 if ok else 1.0])
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            check = ("bit-exact on every rank (%s of the global array rebuilt from each rank's seed)" % ops[0][0]
+                     if float(flag.item()) == 0.0 else "MISMATCH on at least one rank")
+
         # On one GPU the swap call is the one permute launch, so only the kernel's
         # own event pair is recorded (each extra stream event adds a few us between
         # the kernels); across GPUs the call's pair brackets the whole exchange.
@@ -517,6 +565,7 @@ def main():
             },
         }
         if world > 1:
+            line["exchange_check"] = check
             G = world
             xport = "RCCL" if backend == "nccl" else "%s (host-staged rehearsal)" % backend
             n_rank = ops[0][2] / 2                        # bytes held per rank

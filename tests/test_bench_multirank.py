@@ -94,6 +94,10 @@ def _body(rank, world):
             assert k2v.split == 2 and v2k.split == 4
             assert np.asarray(k2v.unchunk().toarray()).tobytes() == full.tobytes()
             assert np.asarray(v2k.unchunk().toarray()).tobytes() == full.tobytes()
+        # bench.py's post-timing check of the exchange, on shards made the bench's way
+        t = bench.synth_shard(torch, shape, dt, torch.device("cpu"), 1234 + rank)
+        tb = ConstructMI355X.fromshards(t.reshape(-1).view(torch.uint8), gshape, context=ctx, split=split, dtype=dt)
+        assert bench.exchange_check(torch, cfg, tb, ctx, torch.device("cpu"), shape, dt, split), cfg
 
 
 def _worker(rank, world, port, errq):
