@@ -211,35 +211,43 @@ def main():
     ap.add_argument("--ops", default=",".join(OPS))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--placements", type=int, default=1, help="separate buffer allocations per op")
     ap.add_argument("--check", action="store_true", help="compare every library's permute output with torch's")
     a = ap.parse_args()
     libs = [load(p) for p in a.libs]
     for name in a.ops.split(","):
-        op = OPS[name]()
-        times = [[] for _ in libs]
-        for _ in range(2):
-            for k, lib in enumerate(libs):
-                op(lib)
-                if a.check and hasattr(op, "check") and _ == 0:
-                    op.dst.fill_(0)
+        # --placements K: K separate allocations of the op's buffers (buffer
+        # placement moves these kernels by up to ~25%, profiles/r03d_alloc_kind.log),
+        # every library timed on every one, interleaved
+        insts = [OPS[name]() for _ in range(a.placements)]
+        times = [[[] for _ in libs] for _ in insts]
+        for j, op in enumerate(insts):
+            for _ in range(2):
+                for k, lib in enumerate(libs):
                     op(lib)
-                    torch.cuda.synchronize()
-                    if not op.check():
-                        print("%-14s %-40s OUTPUT MISMATCH" % (name, a.libs[k].split("/")[-1]), flush=True)
+                    if a.check and hasattr(op, "check") and _ == 0 and j == 0:
+                        op.dst.fill_(0)
+                        op(lib)
+                        torch.cuda.synchronize()
+                        if not op.check():
+                            print("%-14s %-40s OUTPUT MISMATCH" % (name, a.libs[k].split("/")[-1]), flush=True)
         for _ in range(a.rounds):
-            for k, lib in enumerate(libs):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.reps):
-                    op(lib)
-                e1.record()
-                e1.synchronize()
-                times[k].append(e0.elapsed_time(e1) / a.reps)
-        for k, p in enumerate(a.libs):
-            ms = float(np.median(times[k]))
-            print("%-14s %-40s %8.4f ms  %8.1f GB/s  (min %.4f)" % (name, p.split("/")[-1], ms,
-                  op.bytes / ms / 1e6, min(times[k])), flush=True)
-        del op
+            for j, op in enumerate(insts):
+                for k, lib in enumerate(libs):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(a.reps):
+                        op(lib)
+                    e1.record()
+                    e1.synchronize()
+                    times[j][k].append(e0.elapsed_time(e1) / a.reps)
+        for j, op in enumerate(insts):
+            for k, p in enumerate(a.libs):
+                ms = float(np.median(times[j][k]))
+                tag = name if a.placements == 1 else "%s#%d" % (name, j)
+                print("%-14s %-40s %8.4f ms  %8.1f GB/s  (min %.4f)" % (tag, p.split("/")[-1], ms,
+                      op.bytes / ms / 1e6, min(times[j][k])), flush=True)
+        del insts, op
         torch.cuda.empty_cache()
 
 

@@ -133,6 +133,51 @@ def make_ops():
     return ops
 
 
+def matrix(a, ops):
+    """--matrix K: K source and K destination hipMalloc buffers, every (source,
+    destination) pair timed: is a slow placement a property of one buffer or
+    of the pair?"""
+    for name in a.ops.split(","):
+        sb, db, algo, run = ops[name]()
+        srcs, dsts = [], []
+        for _ in range(a.matrix):
+            s, _n = alloc("hipmalloc", sb, 0)
+            d, _n = alloc("hipmalloc", db, 0)
+            assert s and d
+            assert hip.hipMemset(ctypes.c_void_p(s), 7, sb) == 0 and hip.hipMemset(ctypes.c_void_p(d), 0, db) == 0
+            srcs.append(s)
+            dsts.append(d)
+        hip.hipDeviceSynchronize()
+        K = a.matrix
+        t = np.zeros((K, K))
+        for i in range(K):
+            for j in range(K):
+                run(srcs[i], dsts[j])
+                run(srcs[i], dsts[j])
+        torch.cuda.synchronize()
+        res = [[[] for _ in range(K)] for _ in range(K)]
+        for _ in range(a.rounds):
+            for i in range(K):
+                for j in range(K):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(a.reps):
+                        run(srcs[i], dsts[j])
+                    e1.record()
+                    e1.synchronize()
+                    res[i][j].append(e0.elapsed_time(e1) / a.reps)
+        for i in range(K):
+            for j in range(K):
+                t[i, j] = np.median(res[i][j])
+        print("%s: ms by (source row, destination column); frac of 8 TB/s in brackets" % name, flush=True)
+        for i in range(K):
+            print("  src 0x%x  " % srcs[i] + "  ".join("%.4f (%.3f)" % (t[i, j], algo / t[i, j] / 1e6 / 8000)
+                                                     for j in range(K)), flush=True)
+        print("  dst " + "  ".join("0x%x" % d for d in dsts), flush=True)
+        for p_ in srcs + dsts:
+            hip.hipFree(ctypes.c_void_p(p_))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
@@ -140,6 +185,7 @@ def main():
     ap.add_argument("--ops", default="c5_pack,c5_v2k,c5_T,c3_T1024,c2_swap")
     ap.add_argument("--kinds", default="hipmalloc,contiguous,vmm,hipmalloc2")
     ap.add_argument("--vmm-chunk", type=int, default=1 << 30)
+    ap.add_argument("--matrix", type=int, default=0, help="K sources x K destinations (hipMalloc) per op")
     a = ap.parse_args()
     torch.cuda.init()
     hip.hipMemGetAllocationGranularity.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p, ctypes.c_int]
@@ -151,6 +197,8 @@ def main():
                               ctypes.c_ulonglong]
     hip.hipMemSetAccess.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
     ops = make_ops()
+    if a.matrix:
+        return matrix(a, ops)
     for name in a.ops.split(","):
         sb, db, algo, run = ops[name]()
         bufs = {}

@@ -8,5 +8,5 @@ export TMPDIR=/tmp
 NAME=${NAME:-ab}
 OPS=${OPS:-c2_swap,c5_T,c5_perm,c3_T,c3_swap}
 ROUNDS=${ROUNDS:-7}
-timeout -k 10 ${LIMIT:-700} python tools/ab_bench.py bolt_amd/libbolt_mi355x.so "$@" --ops $OPS --rounds $ROUNDS --check > gpurun_out/ab_$NAME.log 2>&1 || { echo AB_FAIL; tail -20 gpurun_out/ab_$NAME.log; exit 1; }
+timeout -k 10 ${LIMIT:-700} python tools/ab_bench.py bolt_amd/libbolt_mi355x.so "$@" --ops $OPS --rounds $ROUNDS --placements ${PLACEMENTS:-1} --check > gpurun_out/ab_$NAME.log 2>&1 || { echo AB_FAIL; tail -20 gpurun_out/ab_$NAME.log; exit 1; }
 cat gpurun_out/ab_$NAME.log
