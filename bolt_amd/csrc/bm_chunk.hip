@@ -36,22 +36,6 @@ constexpr int64_t kStageBytes = 32768;   // LDS per tile when records are small 
 constexpr int64_t kMaxStageBytes = 65536;
 constexpr int kMaxParts = 8;
 
-#ifndef BM_RECMAP_SPREAD
-#define BM_RECMAP_SPREAD 0  // log2 of the stripes the tile order is spread over (0 = in order; A/B knob)
-#endif
-// Tile order: with stripes S = 2^BM_RECMAP_SPREAD, consecutive tiles (the
-// blocks resident at the same time) are taken from S equal stripes of the
-// record range instead of one contiguous window, so the bytes in flight are
-// spread over the whole buffer's pages.  A bijection on the first S*floor(n/S)
-// tiles; the remainder stays in order.
-__device__ __forceinline__ int64_t spread_tile(int64_t t, int64_t n) {
-  if (BM_RECMAP_SPREAD <= 0) return t;
-  constexpr int64_t S = (int64_t)1 << (BM_RECMAP_SPREAD > 0 ? BM_RECMAP_SPREAD : 0);
-  const int64_t per = n >> (BM_RECMAP_SPREAD > 0 ? BM_RECMAP_SPREAD : 0);
-  if (per == 0 || t >= per * S) return t;
-  return (t & (S - 1)) * per + (t >> (BM_RECMAP_SPREAD > 0 ? BM_RECMAP_SPREAD : 0));
-}
-
 template <int ES> struct Elem;
 template <> struct Elem<1> { typedef uint8_t t; };
 template <> struct Elem<2> { typedef uint16_t t; };
@@ -107,8 +91,7 @@ __global__ void __launch_bounds__(kCThreads)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = (nrec + rb - 1) / rb;
-  for (int64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-    const int64_t t = spread_tile(t0, ntiles);
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t r0 = t * rb;
     const int64_t nr = min(rb, nrec - r0);
     // stage nr contiguous source records
@@ -163,9 +146,8 @@ __global__ void __launch_bounds__(kCThreads)
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = nrec * P.n;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t r0 = t / P.n;
-    const int p = (int)(t - r0 * P.n);
-    const int64_t r = spread_tile(r0, nrec);
+    const int64_t r = t / P.n;
+    const int p = (int)(t - r * P.n);
     const int64_t slo = P.slo[p], dlo = P.dlo[p];
     stage_lds(reinterpret_cast<L *>(smem), reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES),
               (P.shi[p] - slo) * ES / LB);
