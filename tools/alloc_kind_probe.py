@@ -49,6 +49,24 @@ class AccessDesc(ctypes.Structure):
     _fields_ = [("loc_type", ctypes.c_int), ("loc_id", ctypes.c_int), ("flags", ctypes.c_int)]
 
 
+_VMM = {}  # base -> (size, [handles]) for vmm_free
+
+
+def vmm_free(base):
+    size, handles, ch = _VMM.pop(base)
+    hip.hipMemUnmap(ctypes.c_void_p(base), ctypes.c_size_t(size))
+    for h in handles:
+        hip.hipMemRelease(h)
+    hip.hipMemAddressFree(ctypes.c_void_p(base), ctypes.c_size_t(size))
+
+
+def free(kind, p):
+    if kind == "vmm":
+        vmm_free(p)
+    else:
+        hip.hipFree(ctypes.c_void_p(p))
+
+
 def alloc(kind, nbytes, chunk):
     p = ctypes.c_void_p()
     if kind.startswith("hipmalloc"):
@@ -68,6 +86,7 @@ def alloc(kind, nbytes, chunk):
                                 ctypes.c_ulonglong(0)) != 0:
         return None, "reserve failed"
     off = 0
+    handles = []
     while off < size:
         h = ctypes.c_void_p()
         rc = hip.hipMemCreate(ctypes.byref(h), ctypes.c_size_t(ch), ctypes.byref(prop), ctypes.c_ulonglong(0))
@@ -77,7 +96,9 @@ def alloc(kind, nbytes, chunk):
                            ctypes.c_ulonglong(0))
         if rc != 0:
             return None, "hipMemMap rc %d" % rc
+        handles.append(h)
         off += ch
+    _VMM[p.value] = (size, handles, ch)
     acc = AccessDesc(loc_type=1, loc_id=0, flags=3)
     if hip.hipMemSetAccess(p, ctypes.c_size_t(size), ctypes.byref(acc), ctypes.c_size_t(1)) != 0:
         return None, "hipMemSetAccess failed"
@@ -140,10 +161,11 @@ def matrix(a, ops):
     for name in a.ops.split(","):
         sb, db, algo, run = ops[name]()
         srcs, dsts = [], []
-        for _ in range(a.matrix):
-            s, _n = alloc("hipmalloc", sb, 0)
-            d, _n = alloc("hipmalloc", db, 0)
-            assert s and d
+        kinds = (a.matrix_kinds.split(",") * a.matrix)[:a.matrix]
+        for kind in kinds:
+            s, _n = alloc(kind, sb, a.vmm_chunk)
+            d, _n = alloc(kind, db, a.vmm_chunk)
+            assert s and d, (kind, _n)
             assert hip.hipMemset(ctypes.c_void_p(s), 7, sb) == 0 and hip.hipMemset(ctypes.c_void_p(d), 0, db) == 0
             srcs.append(s)
             dsts.append(d)
@@ -169,13 +191,15 @@ def matrix(a, ops):
         for i in range(K):
             for j in range(K):
                 t[i, j] = np.median(res[i][j])
-        print("%s: ms by (source row, destination column); frac of 8 TB/s in brackets" % name, flush=True)
+        print("%s: ms by (source row, destination column); frac of 8 TB/s in brackets; kinds %s"
+              % (name, ",".join(kinds)), flush=True)
         for i in range(K):
             print("  src 0x%x  " % srcs[i] + "  ".join("%.4f (%.3f)" % (t[i, j], algo / t[i, j] / 1e6 / 8000)
                                                      for j in range(K)), flush=True)
         print("  dst " + "  ".join("0x%x" % d for d in dsts), flush=True)
-        for p_ in srcs + dsts:
-            hip.hipFree(ctypes.c_void_p(p_))
+        for k_, (s_, d_) in zip(kinds, zip(srcs, dsts)):
+            free(k_, s_)
+            free(k_, d_)
 
 
 def main():
@@ -185,7 +209,8 @@ def main():
     ap.add_argument("--ops", default="c5_pack,c5_v2k,c5_T,c3_T1024,c2_swap")
     ap.add_argument("--kinds", default="hipmalloc,contiguous,vmm,hipmalloc2")
     ap.add_argument("--vmm-chunk", type=int, default=1 << 30)
-    ap.add_argument("--matrix", type=int, default=0, help="K sources x K destinations (hipMalloc) per op")
+    ap.add_argument("--matrix", type=int, default=0, help="K sources x K destinations per op")
+    ap.add_argument("--matrix-kinds", default="hipmalloc", help="allocation kinds of the matrix buffers, cycled")
     a = ap.parse_args()
     torch.cuda.init()
     hip.hipMemGetAllocationGranularity.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p, ctypes.c_int]
@@ -196,6 +221,9 @@ def main():
     hip.hipMemMap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
                               ctypes.c_ulonglong]
     hip.hipMemSetAccess.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    hip.hipMemUnmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    hip.hipMemRelease.argtypes = [ctypes.c_void_p]
+    hip.hipMemAddressFree.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     ops = make_ops()
     if a.matrix:
         return matrix(a, ops)
@@ -230,11 +258,9 @@ def main():
             print("%-10s %-12s %8.4f ms  %7.1f GB/s  frac %.3f  (min %.4f, max %.4f)  src 0x%x dst 0x%x  %s"
                   % (name, k, ms, algo / ms / 1e6, algo / ms / 1e6 / 8000, min(times[k]), max(times[k]), s, d,
                      note or ""), flush=True)
-        # buffers are leaked on purpose (VMM unmapping is not needed for a probe); free plain ones
         for k, (s, d, _) in bufs.items():
-            if k.startswith("hipmalloc") or k == "contiguous":
-                hip.hipFree(ctypes.c_void_p(s))
-                hip.hipFree(ctypes.c_void_p(d))
+            free(k, s)
+            free(k, d)
 
 
 if __name__ == "__main__":
