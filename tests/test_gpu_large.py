@@ -258,3 +258,31 @@ def test_getitem_full_size_c2(gpu_ctx):
     # sorted keys: the reference's record order is the listed order only within a key's run
     assert r.shape == (1 << 20,) and r.split == 1
     assert torch.equal(r._data.view(torch.float32), x.reshape(-1)[lin])
+
+
+def test_c1_step_against_oracle(gpu_ctx):
+    """BASELINE C1 (the reference's CPU-runnable case), the whole bench step:
+    float64 (100,64,64) N(0,1) (seed 0, as SURVEY 8(d)), swap((0,),(0,)), then
+    sum / mean / var / std at axis=None and axis=(0,) of the swapped array,
+    against the oracle's record-level restatement of the Spark path (8
+    partitions): the swap bit for bit, the statistics by the stat_close rule
+    (rtol 1e-12 for float64)."""
+    import golden_cases as G
+    from oracle import bolt_oracle as O
+    x = np.random.default_rng(0).standard_normal((100, 64, 64))
+    b = bolt.array(x, gpu_ctx, axis=(0,))
+    s = b.swap((0,), (0,))
+    rs = O.swap(O.parallelize(x, axis=(0,), npartitions=8), (0,), (0,))
+    assert s.shape == (64, 100, 64) and s.split == 1
+    assert s.toarray().tobytes() == O.toarray(rs).tobytes()
+    y = x.transpose(1, 0, 2)
+    for name in ("sum", "mean", "var", "std"):
+        for ax in (None, (0,)):
+            got = getattr(s, name)(axis=ax)
+            if name == "sum":
+                want = O.sum_(rs, ax)
+            else:
+                want = O.stat(rs, {"var": "variance", "std": "stdev"}.get(name, name), ax)
+            truth = G.truth_stat(y, name, ax)
+            assert np.asarray(got).dtype == np.asarray(want).dtype, (name, ax)
+            assert G.stat_close(got, want, truth, np.float64, y, name), (name, ax)
