@@ -53,6 +53,17 @@ struct Parts {
 #ifndef BM_STAGE_U
 #define BM_STAGE_U 8
 #endif
+#ifndef BM_RECMAP_NT
+#define BM_RECMAP_NT 3  // bit 0: non-temporal staging loads, bit 1: non-temporal stores (A/B knob)
+#endif
+template <typename V> __device__ __forceinline__ V ld_src(const V *p) {
+  if (BM_RECMAP_NT & 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <typename V> __device__ __forceinline__ void st_dst(V v, V *p) {
+  if (BM_RECMAP_NT & 2) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 #ifndef BM_GATHER_U
 #define BM_GATHER_U 0  // 0: 16 B of map per lane per round
 #endif
@@ -64,7 +75,7 @@ __device__ __forceinline__ void stage_lds(L *sl, const L *s, int64_t n) {
 #pragma unroll
     for (int u = 0; u < kStageU; ++u) {
       const int64_t i = i0 + (int64_t)u * kCThreads;
-      if (i < n) v[u] = __builtin_nontemporal_load(s + i);
+      if (i < n) v[u] = ld_src(s + i);
     }
 #pragma unroll
     for (int u = 0; u < kStageU; ++u) {
@@ -126,7 +137,7 @@ __global__ void __launch_bounds__(kCThreads)
           for (int k = 0; k < VEC; ++k) v[k] = lds[rb_[u] + m[u][k]];
           V w;
           __builtin_memcpy(&w, v, sizeof(V));
-          __builtin_nontemporal_store(w, d + i);
+          st_dst(w, d + i);
         }
       }
     }
@@ -175,7 +186,7 @@ __global__ void __launch_bounds__(kCThreads)
           for (int k = 0; k < VEC; ++k) v[k] = lds[m[u][k] - slo];
           V w;
           __builtin_memcpy(&w, v, sizeof(V));
-          __builtin_nontemporal_store(w, d + i);
+          st_dst(w, d + i);
         }
       }
     }
