@@ -79,7 +79,13 @@ constexpr int kThreads = 256;
 #define BM_RC_SKEW 0  // rowcopy: diagonal row walk when the fastest row dim's source step is >= this many bytes (0 = off; A/B knob)
 #endif
 #ifndef BM_RC_SKEW_MAXB
-#define BM_RC_SKEW_MAXB 256  // ... and rows are at most this many bytes (longer rows already spread over L2 channels)
+// ... and rows are at most this many bytes.  Round 3 extended the diagonal
+// tiles from 256-B to 4-KiB rows (profiles/r03k_ab_diag_c4.log,
+// r03l_ab_diag_rows.log, every placement): C4 swap (2-KiB rows) 7.40 ->
+// 6.77-6.83 ms (+8.5-9.4%), 4-KiB rows +10-11%, 1 KiB +5%, 512 B +2-3%;
+// 16-KiB rows lose 2-9% (a 16x16 tile then spans 4 MiB per side), so they
+// keep row order.
+#define BM_RC_SKEW_MAXB 4096
 #endif
 #ifndef BM_RC_DIAG
 #define BM_RC_DIAG 65536  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this many bytes (0 = off): C3 +8-9%, 64 GiB target +13-15% (profiles/r02_ab_diag.log)
@@ -692,7 +698,7 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)outer.size());
     return BM_E_ARG;
   }
-  if (row_bytes <= BM_RC_SKEW_MAXB) set_skew(d, outer, es, BM_RC_SKEW);
+  if (row_bytes <= 256) set_skew(d, outer, es, BM_RC_SKEW);  // (A/B knob, off)
   Diag16 dg{};
   {
     // 16x16 diagonal tiles when the fastest row dim steps the source by a

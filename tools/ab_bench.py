@@ -193,6 +193,11 @@ OPS = {
     "u8_T": lambda: Permute((2000, 1024, 2048), (2, 1, 0), np.uint8),
     "u16_2d": lambda: Permute((2000, 1048576), (1, 0), np.uint16),
     "c4_swap": lambda: Permute((2000, 1024, 1024), (1, 0, 2), np.uint16),
+    "rc_512": lambda: Permute((8192, 2048, 128), (1, 0, 2), np.float32),
+    "rc_1k": lambda: Permute((8192, 1024, 256), (1, 0, 2), np.float32),
+    "rc_4k": lambda: Permute((4096, 512, 1024), (1, 0, 2), np.float32),
+    "rc_16k": lambda: Permute((2048, 256, 4096), (1, 0, 2), np.float32),
+    "rc_c4half": lambda: Permute((5008, 1024, 1024), (1, 0, 2), np.uint16),
     "t64_mean_cols": lambda: Reduce(0, 1, 4096, 2097152, np.float32, np.float32),
     "t64_std_cols": lambda: Reduce(2, 1, 4096, 2097152, np.float32, np.float32),
     "t64f_mean_cols": lambda: Reduce(0, 1, 8192, 2097152, np.float32, np.float32),
