@@ -90,6 +90,9 @@ constexpr int kThreads = 256;
 #ifndef BM_RC_DIAG
 #define BM_RC_DIAG 65536  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this many bytes (0 = off): C3 +8-9%, 64 GiB target +13-15% (profiles/r02_ab_diag.log)
 #endif
+#ifndef BM_RC_DIAG_LOG2
+#define BM_RC_DIAG_LOG2 4  // Diag16: 2^4 x 2^4 diagonal tiles (A/B knob)
+#endif
 #ifndef BM_RC_DIAG_GFAST
 // rowcopy Diag16 tile order: 1 = the g-tiles (the next-fastest row dim, e.g.
 // C3's k, 128-B source step) vary fastest between consecutive tiles, so the
@@ -149,7 +152,9 @@ struct Diag16 {
 __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   const uint64_t outer = fd_div(row, t.grp);
   const uint64_t q = row - outer * t.grp.d;
-  const uint64_t tile = q >> 8, w = q & 255;
+  constexpr int L = BM_RC_DIAG_LOG2;
+  constexpr uint64_t D = 1ull << L;
+  const uint64_t tile = q >> (2 * L), w = q & (D * D - 1);
   uint64_t gt, ct;
   if (BM_RC_DIAG_GFAST) {
     ct = fd_div(tile, t.ntg);
@@ -158,8 +163,8 @@ __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
     gt = fd_div(tile, t.ntc);
     ct = tile - gt * t.ntc.d;
   }
-  const uint64_t j = w >> 4, k = w & 15;
-  const uint64_t g = gt * 16 + k, c = ct * 16 + ((k + j) & 15);
+  const uint64_t j = w >> L, k = w & (D - 1);
+  const uint64_t g = gt * D + k, c = ct * D + ((k + j) & (D - 1));
   return outer * t.grp.d + g * t.nc + c;
 }
 
@@ -706,12 +711,13 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     const int n = (int)outer.size();
     if (BM_RC_DIAG && row_bytes <= BM_RC_SKEW_MAXB && n >= 2 && d.skew == 0) {
       const Dim &f = outer[n - 1], &g = outer[n - 2];
-      if (f.n % 16 == 0 && g.n % 16 == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
+      constexpr int64_t D = (int64_t)1 << BM_RC_DIAG_LOG2;
+      if (f.n % D == 0 && g.n % D == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
           std::llabs(g.ss) < std::llabs(f.ss)) {
         dg.on = 1;
         dg.grp = make_fastdiv((uint64_t)(f.n * g.n));
-        dg.ntc = make_fastdiv((uint64_t)(f.n / 16));
-        dg.ntg = make_fastdiv((uint64_t)(g.n / 16));
+        dg.ntc = make_fastdiv((uint64_t)(f.n / D));
+        dg.ntg = make_fastdiv((uint64_t)(g.n / D));
         dg.nc = (uint64_t)f.n;
       }
     }
