@@ -91,7 +91,7 @@ constexpr int kThreads = 256;
 #define BM_RC_DIAG 65536  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this many bytes (0 = off): C3 +8-9%, 64 GiB target +13-15% (profiles/r02_ab_diag.log)
 #endif
 #ifndef BM_RC_DIAG_LOG2
-#define BM_RC_DIAG_LOG2 4  // Diag16: 2^4 x 2^4 diagonal tiles (A/B knob)
+#define BM_RC_DIAG_LOG2 0  // diagonal tile side 2^k (0: by row size, 8x8 up to 1 KiB rows, else 16x16; A/B knob)
 #endif
 #ifndef BM_RC_DIAG_GFAST
 // rowcopy Diag16 tile order: 1 = the g-tiles (the next-fastest row dim, e.g.
@@ -142,7 +142,7 @@ constexpr int kUnroll = BM_RC_UNROLL;
 // (tools/skew/rowcopy_skew.hip "diag16").  A bijection inside each tile.
 struct Diag16 {
   int on;
-  int pad_;
+  int lg;        // log2 of the tile side (3: 8x8, 4: 16x16)
   FastDiv grp;   // Ng * Nc rows per (outer) group
   FastDiv ntc;   // Nc / 16 tiles along c
   FastDiv ntg;   // Ng / 16 tiles along g
@@ -152,8 +152,8 @@ struct Diag16 {
 __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   const uint64_t outer = fd_div(row, t.grp);
   const uint64_t q = row - outer * t.grp.d;
-  constexpr int L = BM_RC_DIAG_LOG2;
-  constexpr uint64_t D = 1ull << L;
+  const int L = t.lg;
+  const uint64_t D = 1ull << L;
   const uint64_t tile = q >> (2 * L), w = q & (D * D - 1);
   uint64_t gt, ct;
   if (BM_RC_DIAG_GFAST) {
@@ -711,10 +711,16 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     const int n = (int)outer.size();
     if (BM_RC_DIAG && row_bytes <= BM_RC_SKEW_MAXB && n >= 2 && d.skew == 0) {
       const Dim &f = outer[n - 1], &g = outer[n - 2];
-      constexpr int64_t D = (int64_t)1 << BM_RC_DIAG_LOG2;
+      // 8x8 tiles for rows up to 1 KiB, 16x16 above (profiles/r03n_ab_diagsize.log,
+      // r03o_ab_diag8_*.log: 8x8 on C3's 128-B rows +4.3-6.1% on three
+      // placements, 1-KiB rows +2%, the 64 GiB target -0.4..-1.8%; on 2-4-KiB
+      // rows 16x16 is equal or +1%; 32x32 loses everywhere)
+      const int lg = BM_RC_DIAG_LOG2 > 0 ? BM_RC_DIAG_LOG2 : (row_bytes <= 1024 ? 3 : 4);
+      const int64_t D = (int64_t)1 << lg;
       if (f.n % D == 0 && g.n % D == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
           std::llabs(g.ss) < std::llabs(f.ss)) {
         dg.on = 1;
+        dg.lg = lg;
         dg.grp = make_fastdiv((uint64_t)(f.n * g.n));
         dg.ntc = make_fastdiv((uint64_t)(f.n / D));
         dg.ntg = make_fastdiv((uint64_t)(g.n / D));
