@@ -97,6 +97,12 @@ def test_permute_all_perms_4d(dtype):
     ((64, 32, 64, 8), (1, 2, 0, 3)),
     ((32, 4, 16, 32, 16), (1, 2, 3, 0, 4)),
     ((48, 20, 40, 8), (1, 2, 0, 3)),
+    # round 3: diagonal tiles by row size -- 8x8 up to 1-KiB rows, 16x16 for
+    # 1-4-KiB rows (C4's 2-KiB rows), row order beyond 4 KiB or when an
+    # extent is not a multiple of the tile side
+    ((64, 128, 256), (1, 0, 2)),
+    ((40, 24, 8, 512), (1, 2, 0, 3)),
+    ((24, 16, 1024), (1, 0, 2)),
 ])
 @pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64, np.complex128])
 def test_permute_shapes(shape, perm, dtype):
