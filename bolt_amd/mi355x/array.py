@@ -963,6 +963,25 @@ class BoltArrayMI355X(BoltArray):
         for i, key in enumerate(np.ndindex(*kshape)):
             yield tuple(int(k) for k in key), flat[i]
 
+    def display(self):
+        """Print the first 10 records as (key, value) pairs, as the Spark
+        mode's ``rdd.take(10)`` does (array.py:1022-1027).  Only the
+        leading-axis rows that hold them leave the GPU; every rank takes part
+        in the gather, rank 0 prints (the driver's console in Spark)."""
+        kshape = self._shape[:self._split]
+        nrec = int(np.prod(kshape, dtype=np.int64))
+        n = min(10, nrec)
+        if n == 0:
+            return
+        per_row = int(np.prod(kshape[1:], dtype=np.int64))
+        rows = -(-n // per_row)
+        part = self if rows >= self._shape[0] else self[0:rows]
+        for i, rec in enumerate(part.records()):
+            if i >= n:
+                break
+            if self._ctx.rank == 0:
+                print(rec)
+
     def tordd(self):
         from bolt_amd.mi355x.records import RecordView
         return RecordView(list(self.records()), self._npartitions or self._ctx.world_size,

@@ -246,3 +246,20 @@ def test_empty_reductions(bctx):
     assert c.mean(axis=0).shape == (0, 4) and c.std(axis=0).shape == (0, 4)
     assert c.swap((0,), (0,)).shape == (0, 3, 4)
     assert exact(c.T.toarray(), np.zeros((4, 0, 3), np.float32))
+
+
+def test_display(bctx, capsys):
+    """display() prints rdd.take(10): the first 10 (key, value) records in key
+    order (spark/array.py:1022-1027)."""
+    x = np.arange(4 * 5 * 3).reshape((4, 5, 3)).astype(np.float32)
+    b = bolt.array(x, bctx, axis=(0, 1))
+    b.display()
+    want = []
+    for i, key in enumerate(np.ndindex(4, 5)):
+        if i == 10:
+            break
+        want.append(str((key, x[key])))
+    assert capsys.readouterr().out.splitlines() == "\n".join(want).splitlines()
+    small = bolt.array(x[:1, :3], bctx, axis=(0, 1))
+    small.display()
+    assert len(capsys.readouterr().out.strip().splitlines()) == 3
