@@ -117,6 +117,16 @@ constexpr int kThreads = 256;
 #ifndef BM_TR_XCD
 #define BM_TR_XCD 0  // transpose: the blocks one XCD runs take a contiguous eighth of the tiles (A/B knob)
 #endif
+#ifndef BM_TR_ASPREAD
+// fused transposes (short source-contiguous axis fused with its continuation,
+// C3's .T): the a-tiles of consecutive tiles are spread S ways over the fused
+// source rows (ta -> (ta % S) * (ntA / S) + ta / S) when ntA >= 2 S.  A/B on
+// six placements (profiles/r03q_ab_asp_c3full.log): C3 .T S = 32 +0.7..+2.0%
+// at full size, +4.2..+5.5% at 1024 rows; S = 16 / 64 smaller or mixed.  The
+// unfused C2 swap loses 12-23% with any S (r03q_ab_asp_c2_c3.log): its tiles
+// in flight share DRAM pages of one contiguous window, so it stays in order.
+#define BM_TR_ASPREAD 32
+#endif
 #ifndef BM_TR_LOOP
 #define BM_TR_LOOP 0  // transpose: each block walks the batch dim that is page-local on both sides, if >= this many blocks remain (0 = off; A/B knob)
 #endif
@@ -220,6 +230,8 @@ struct TransDesc {
   FastDiv Lb1, La1;
   int64_t sb2, da2;
   uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (BM_TR_XCD)
+  FastDiv asp;     // BM_TR_ASPREAD: S (1 = off)
+  uint64_t aspq;   // ntA / S
 };
 
 // TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
@@ -271,11 +283,15 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t t = d.xcd8 ? (t0 % 8) * d.xcd8 + t0 / 8 : t0;
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
-    const uint64_t ta = fd_div(rem, d.ntB);
+    uint64_t ta = fd_div(rem, d.ntB);
     uint64_t tb = rem - ta * d.ntB.d;
     if (BM_TR_ROT) {
       tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
       if (tb >= d.ntB.d) tb -= d.ntB.d;
+    }
+    if (BM_TR_ASPREAD && d.asp.d > 1) {
+      const uint64_t hi = fd_div(ta, d.asp);
+      ta = (ta - hi * d.asp.d) * d.aspq + hi;
     }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
@@ -965,6 +981,12 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   td.ntB = make_fastdiv(ntB);
   td.ntAB = make_fastdiv(ntA * ntB);
   td.ntiles = ntA * ntB * nb;
+  td.asp = make_fastdiv(1);
+  td.aspq = ntA;
+  if (BM_TR_ASPREAD > 1 && fused && ntA % BM_TR_ASPREAD == 0 && ntA >= 2 * BM_TR_ASPREAD) {
+    td.asp = make_fastdiv(BM_TR_ASPREAD);
+    td.aspq = ntA / BM_TR_ASPREAD;
+  }
   td.xcd8 = (BM_TR_XCD && td.ntiles % 8 == 0 && td.ntiles / loop_n <= kMaxGrid && loop_n == 1) ? td.ntiles / 8 : 0;
   // 16-B vectors when every source row start (dims other than a) and every
   // destination row start (dims other than b) is 16-B aligned.

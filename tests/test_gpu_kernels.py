@@ -90,6 +90,11 @@ def test_permute_all_perms_4d(dtype):
     # float64 with 512-B destination rows read from nearby source rows: fused
     # with the continuation, 32 x 128 tiles, a ragged last tile (BM_T8_FUSE512)
     ((5, 3, 7, 64, 64), (2, 0, 4, 1, 3)),
+    # fused float32 .T with >= 64 a-tiles: a-tiles spread 32 ways (BM_TR_ASPREAD),
+    # a ragged destination axis, and 32 a-tiles (in order)
+    ((6, 4, 256, 32), (3, 2, 1, 0)),
+    ((7, 3, 128, 32), (3, 2, 1, 0)),
+    ((5, 3, 64, 32), (3, 2, 1, 0)),
     ((6, 64, 5, 64), (2, 0, 3, 1)),
     # short rows whose fastest row dim strides the source by >= 64 KiB: the
     # rowcopy walks 16x16 diagonal tiles (Diag16), with and without outer dims,
