@@ -35,6 +35,9 @@ constexpr int kCThreads = 256;
 constexpr int64_t kStageBytes = 32768;   // LDS per tile when records are small (5 blocks / CU)
 constexpr int64_t kMaxStageBytes = 65536;
 constexpr int kMaxParts = 8;
+#ifndef BM_RECMAP_GRIDCAP
+#define BM_RECMAP_GRIDCAP 16384  // blocks per launch, then grid-stride over tiles (A/B knob)
+#endif
 
 template <int ES> struct Elem;
 template <> struct Elem<1> { typedef uint8_t t; };
@@ -326,7 +329,7 @@ extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int6
       L.shmem = (size_t)(rb * rec_bytes + 15) / 16 * 16;
       ntiles = (nrec + rb - 1) / rb;
     }
-    L.grid = (int)(ntiles < 16384 ? ntiles : 16384);
+    L.grid = (int)(ntiles < BM_RECMAP_GRIDCAP ? ntiles : BM_RECMAP_GRIDCAP);
     const int vec = std::max(1, vb / es);
     switch (es) {
       case 1: launch_lds<1>(L, lb, vec); break;

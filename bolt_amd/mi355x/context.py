@@ -89,7 +89,10 @@ class MI355XContext(object):
         comm = ctypes.c_void_p()
         _lib.check(lib.bm_comm_init(ctypes.byref(comm), self.world_size, uid, self.rank), "bm_comm_init")
         self.comm = comm.value
-        self.comm_stream = torch.cuda.Stream(self.device)
+        # the exchanges run beside the pipelined pack / unpack kernels of the
+        # current stream, whose grids can fill every CU: a high-priority stream
+        # lets RCCL's workgroups dispatch ahead of the copies' queued ones
+        self.comm_stream = torch.cuda.Stream(self.device, priority=-1)
 
     @classmethod
     def _comm_key(cls, ranks):
