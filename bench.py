@@ -49,7 +49,7 @@ CONFIGS = {
            "C3: float32 (4096,256,256,32) per GPU, keys (0,1); swap((0,),(0,)) + .T"),
     "C4": ((10000, 1024, 1024), np.uint16, 1,
            "C4: uint16 (10000,1024,1024) per GPU, key 0; swap((0,),(0,)) + chunk('150') -> unchunk "
-           "+ float64 var over axis 0"),
+           "(plan (73, 1024): the packed layout is the dense one, no bytes move) + float64 var over axis 0"),
     "C5": ((64, 64, 64, 64, 64), np.float64, 3,
            "C5: float64 64^5 per GPU, keys (0,1,2); .T + transpose(2,0,4,1,3) + "
            "chunk((16,16), padding=2) -> unchunk / keys_to_values((2,)) / values_to_keys((0,))"),
@@ -174,11 +174,16 @@ def steps_of(cfg, b, world=1):
     if cfg == "C4":
         from bolt_amd.mi355x.plan import ChunkGeometry, getplan
         plan, pad = getplan(b.shape[1:], b.dtype, "150")
-        P = ChunkGeometry(b.shape[1:], plan, pad).size * (b.shape[0] // world) * s
+        geom = ChunkGeometry(b.shape[1:], plan, pad)
+        P = geom.size * (b.shape[0] // world) * s
+        # chunk('150') splits only the leading value axis of the (1024, 1024)
+        # records: the packed layout IS the dense one, chunk / unchunk are
+        # relabellings that move no bytes (ChunkGeometry.is_identity)
+        moved = 0 if geom.is_identity() else N + P
         ck = {}
         return [("swap", lambda: b.swap((0,), (0,)), 2 * N),
-                ("chunk", lambda: ck.__setitem__("c", b.chunk("150")), N + P),
-                ("unchunk", lambda: ck.pop("c").unchunk(), P + N),
+                ("chunk", lambda: ck.__setitem__("c", b.chunk("150")), moved),
+                ("unchunk", lambda: ck.pop("c").unchunk(), moved),
                 ("var", lambda: b.var(axis=0), N + (n * world // b.shape[0]) * 8)]
     if cfg == "C5":
         from bolt_amd.mi355x.plan import ChunkGeometry

@@ -135,6 +135,10 @@ class ChunkedArrayMI355X(object):
         vshape = shape[split:]
         geom = ChunkGeometry(vshape, plan, padding)
         rec = int(np.prod(vshape, dtype=np.int64))
+        if geom.is_identity():
+            # the packed layout is the dense one: the chunked array shares the
+            # records' bytes (arrays are never written in place)
+            return dense[:nrec * rec * es]
         packed = _empty(nrec * geom.size * es, dense.device)
         if nrec and _use_record_map(rec, es):
             backend.record_gather(dense, 0, packed, 0, nrec, rec, geom.size,
@@ -151,6 +155,8 @@ class ChunkedArrayMI355X(object):
         lshape = local_shape(self._ctx, self._shape)
         nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
         rec = int(np.prod(self.vshape, dtype=np.int64))
+        if self._geom.is_identity():
+            return self._packed[:nrec * rec * es]  # same bytes, dense order
         dense = _empty(nrec * rec * es, self._packed.device)
         if nrec:
             be = self._backend

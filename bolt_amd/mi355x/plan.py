@@ -303,6 +303,21 @@ class ChunkGeometry(object):
     def key(self):
         return (self.vshape, self.plan, self.padding)
 
+    def is_identity(self):
+        """True when the packed record IS the dense record: no padding growth
+        and every chunk box lands at its own dense offset with dense strides
+        (e.g. a plan that splits only the leading value axis, like the default
+        chunk of C4's uint16 (1024, 1024) records, or a single chunk).  Packing
+        and unpacking are then relabellings and move no bytes."""
+        ident = getattr(self, "_identity", None)
+        if ident is None:
+            rec = int(np.prod(self.vshape, dtype=np.int64)) if self.vshape else 1
+            ident = self.size == rec and all(
+                doff == poff and all(n == 1 or a == b for n, a, b in zip(shape, dstr, pstr))
+                for shape, dstr, pstr, doff, poff in self.copies(unpack=False))
+            self._identity = ident
+        return ident
+
 
 def copies_to_map(copies, dst_len):
     """Run strided copies on index arrays: map[dst] = src, as int32.

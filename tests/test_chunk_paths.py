@@ -123,3 +123,45 @@ def test_fused_rechunk_matches_dense_path(bctx, case, dtype, monkeypatch):
         vs = [split + a for a in axes] + [split + a for a in range(len(shape) - split) if a not in axes]
         perm = list(range(split)) + vs
     assert np.asarray(f.unchunk().toarray()).tobytes() == np.ascontiguousarray(x.transpose(perm)).tobytes()
+
+
+def test_identity_geometry_matches_record_map():
+    """ChunkGeometry.is_identity() is exactly "the pack map is the identity"
+    (every chunk box at its own dense offset, nothing padded), over random
+    value shapes, plans and paddings."""
+    import itertools
+    from bolt_amd.mi355x.plan import ChunkGeometry
+    rng = np.random.default_rng(7)
+    seen = {True: 0, False: 0}
+    for _ in range(400):
+        n = int(rng.integers(1, 4))
+        vshape = tuple(int(v) for v in rng.integers(1, 7, n))
+        plan = tuple(int(rng.integers(1, v + 1)) for v in vshape)
+        pad = tuple(int(rng.integers(0, 2)) if rng.random() < 0.3 and p < v else 0
+                    for p, v in zip(plan, vshape))
+        g = ChunkGeometry(vshape, plan, pad)
+        m = g.record_map(unpack=False)
+        want = m.size == int(np.prod(vshape)) and np.array_equal(m, np.arange(m.size))
+        assert g.is_identity() == want, (vshape, plan, pad)
+        seen[want] += 1
+    assert seen[True] > 20 and seen[False] > 20
+    # C4's default chunk: (73, 1024) on (1024, 1024) records moves nothing
+    assert ChunkGeometry((1024, 1024), (73, 1024), (0, 0)).is_identity()
+    assert not ChunkGeometry((64, 64), (16, 16), (2, 2)).is_identity()
+
+
+def test_identity_chunk_shares_bytes(bctx):
+    """chunk / unchunk with an identity geometry alias the records' bytes and
+    still match the reference semantics (chunk contents, round trip)."""
+    x = np.arange(6 * 8 * 5, dtype=np.int16).reshape(6, 8, 5)
+    b = bolt.array(x, bctx, axis=(0,))
+    c = b.chunk((3, 5))
+    assert c._packed.data_ptr() == b._data.data_ptr()
+    u = c.unchunk()
+    assert u._data.data_ptr() == b._data.data_ptr()
+    assert u.toarray().tobytes() == x.tobytes()
+    recs = sorted(c.tordd().collect(), key=lambda kv: kv[0])
+    assert np.array_equal(recs[0][1], x[0, 0:3, :]) and np.array_equal(recs[1][1], x[0, 3:6, :])
+    padded = b.chunk((3, 4), padding=(1, 0))
+    assert padded._packed.data_ptr() != b._data.data_ptr()
+    assert padded.unchunk().toarray().tobytes() == x.tobytes()
