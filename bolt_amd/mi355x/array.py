@@ -277,6 +277,11 @@ class BoltArrayMI355X(BoltArray):
         new_shape = tuple(self._shape[p] for p in perm)
         if perm == list(range(self.ndim)):
             return self._like(self._data, new_shape, split)
+        moved = [p for p in perm if self._shape[p] != 1]
+        if moved == sorted(moved) and (self._ctx.world_size == 1 or perm[0] == 0):
+            # only unit axes move: the C-order bytes are already the result's
+            # (across GPUs the leading axis, hence every slab, stays put)
+            return self._like(self._data, new_shape, split)
         data = permute_sharded(self._ctx, self._backend, self._data, self._shape, perm,
                                self._dtype.itemsize)
         return self._like(data, new_shape, split)

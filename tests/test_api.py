@@ -263,3 +263,18 @@ def test_display(bctx, capsys):
     small = bolt.array(x[:1, :3], bctx, axis=(0, 1))
     small.display()
     assert len(capsys.readouterr().out.strip().splitlines()) == 3
+
+
+def test_permute_of_unit_axes_shares_bytes(bctx):
+    """A permutation that moves only extent-1 axes is a relabelling: same
+    bytes, new shape (swap / transpose results as the reference's)."""
+    x = np.arange(1 * 4 * 1 * 5, dtype=np.float32).reshape(1, 4, 1, 5)
+    b = bolt.array(x, bctx, axis=(0, 1))
+    t = b.transpose(2, 1, 0, 3)
+    assert t._data.data_ptr() == b._data.data_ptr()
+    assert exact(t.toarray(), x.transpose(2, 1, 0, 3))
+    s = b.swap((0,), (0,))
+    assert exact(s.toarray(), x.transpose(1, 2, 0, 3)) and s.split == 2
+    moved = b.transpose(0, 3, 2, 1)
+    assert moved._data.data_ptr() != b._data.data_ptr()
+    assert exact(moved.toarray(), x.transpose(0, 3, 2, 1))
