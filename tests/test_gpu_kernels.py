@@ -358,3 +358,31 @@ def test_host_writable_and_zero_copy_statistics(monkeypatch):
     for (a, name, ax), z, d in zip(cases, got[True], got[False]):
         z, d = np.asarray(z), np.asarray(d)
         assert z.shape == d.shape and z.dtype == d.dtype and z.tobytes() == d.tobytes(), (name, ax)
+
+
+@pytest.mark.parametrize("shape,perm,dtype", [
+    ((600, 4000), (1, 0), np.float32),      # ragged a- and b-tiles
+    ((700, 2048), (1, 0), np.float64),
+    ((3, 520, 1024), (0, 2, 1), np.float32),  # with a batch dim
+])
+def test_adaptive_transpose_order(shape, perm, dtype):
+    """The placement-adaptive order (OrderTuner): call 1 in order, calls 2 / 3
+    time the in-order and the staggered walk, later calls run the faster --
+    every call's output is the same bytes, and the entry gets decided."""
+    import ctypes
+    import torch
+    from bolt_amd.mi355x import _lib
+    lib = _lib.load()
+    assert lib.bm_tune_reset() == 0
+    be = _be()
+    x = _rand(shape, dtype, 11)
+    src = _dev(x)
+    want = np.ascontiguousarray(x.transpose(perm))
+    for call in range(6):
+        out = torch.zeros_like(src)
+        be.permute(src, shape, perm, x.dtype.itemsize, out)
+        torch.cuda.synchronize()
+        assert _host(out, x.dtype, want.shape).tobytes() == want.tobytes(), call
+    summ = (ctypes.c_int64 * 3)()
+    assert lib.bm_tune_summary(summ) == 0
+    assert summ[0] == 1 and summ[1] == 1, list(summ)
