@@ -137,6 +137,12 @@ constexpr int kThreads = 256;
 // (OrderTuner below); 0 = never.
 #define BM_TR_AROT 1
 #endif
+#ifndef BM_TR_AROT_DELTA
+#define BM_TR_AROT_DELTA 0  // extra a-tiles of stagger per b-tile (A/B knob)
+#endif
+#ifndef BM_TR_AROT_FORCE
+#define BM_TR_AROT_FORCE 0  // 1: always the staggered order, no tuner (A/B knob)
+#endif
 #ifndef BM_TR_LOOP
 #define BM_TR_LOOP 0  // transpose: each block walks the batch dim that is page-local on both sides, if >= this many blocks remain (0 = off; A/B knob)
 #endif
@@ -1169,7 +1175,8 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     uint64_t sig = 1469598103934665603ull;
     for (uint64_t x : {ntA, ntB, nb, (uint64_t)TA, (uint64_t)TB, (uint64_t)es, (uint64_t)td.sb, (uint64_t)td.da})
       sig = (sig ^ x) * 1099511628211ull;
-    if (g_order_tuner.pick(src, sig, &t0, &t1)) td.arot = ntA / (ntB * BM_TR_AROT);
+    if (BM_TR_AROT_FORCE || g_order_tuner.pick(src, sig, &t0, &t1))
+      td.arot = (ntA / (ntB * BM_TR_AROT) + BM_TR_AROT_DELTA) % ntA;
   }
   if (t0) (void)hipEventRecord(t0, st);
   int rc = BM_E_ARG;
