@@ -599,6 +599,15 @@ def main():
                 line["xgmi"]["rccl_ms_per_swap"] = round(rccl_ms, 4)
                 line["xgmi"]["rccl_achieved"] = round(payload / (rccl_ms / 1e3) / 1e9, 1)
                 line["xgmi"]["rccl_frac"] = round(payload / (rccl_ms / 1e3) / 1e9 / peak, 4)
+        try:  # the placement-adaptive transpose order's decisions
+            import ctypes
+            from bolt_amd.mi355x import _lib
+            summ = (ctypes.c_int64 * 3)()
+            if _lib.load().bm_tune_summary(summ) == 0:
+                line["roofline"]["order_tuner"] = {"entries": int(summ[0]), "decided": int(summ[1]),
+                                                   "staggered": int(summ[2])}
+        except Exception:
+            pass
         line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
         line["roofline"]["measured_copy_peak"] = HBM_COPY_GBPS
         return line
