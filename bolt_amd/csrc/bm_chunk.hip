@@ -35,6 +35,13 @@ constexpr int kCThreads = 256;
 constexpr int64_t kStageBytes = 32768;   // LDS per tile when records are small (5 blocks / CU)
 constexpr int64_t kMaxStageBytes = 65536;
 constexpr int kMaxParts = 8;
+#ifndef BM_RECMAP_XCDREG
+// 1: the tiles of the blocks dealt to XCD x (blockIdx % 8 under round-robin
+// dispatch) come from the x-th eighth of the records, so the eight XCDs stream
+// eight separate regions at once instead of one contiguous window (A/B knob;
+// applied when the tile count is a multiple of 8)
+#define BM_RECMAP_XCDREG 0
+#endif
 #ifndef BM_RECMAP_GRIDCAP
 #define BM_RECMAP_GRIDCAP 16384  // blocks per launch, then grid-stride over tiles (A/B knob)
 #endif
@@ -105,7 +112,9 @@ __global__ void __launch_bounds__(kCThreads)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = (nrec + rb - 1) / rb;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const bool reg = BM_RECMAP_XCDREG && ntiles % 8 == 0 && gridDim.x % 8 == 0;
+  for (int64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+    const int64_t t = reg ? (t0 % 8) * (ntiles / 8) + t0 / 8 : t0;
     const int64_t r0 = t * rb;
     const int64_t nr = min(rb, nrec - r0);
     // stage nr contiguous source records
@@ -159,7 +168,9 @@ __global__ void __launch_bounds__(kCThreads)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = nrec * P.n;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const bool reg = BM_RECMAP_XCDREG && ntiles % 8 == 0 && gridDim.x % 8 == 0;
+  for (int64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
+    const int64_t t = reg ? (t0 % 8) * (ntiles / 8) + t0 / 8 : t0;
     const int64_t r = t / P.n;
     const int p = (int)(t - r * P.n);
     const int64_t slo = P.slo[p], dlo = P.dlo[p];
