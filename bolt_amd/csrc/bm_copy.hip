@@ -140,6 +140,9 @@ constexpr int kThreads = 256;
 #ifndef BM_TR_AROT_DELTA
 #define BM_TR_AROT_DELTA 0  // extra a-tiles of stagger per b-tile (A/B knob)
 #endif
+#ifndef BM_TR_AROT_FUSED
+#define BM_TR_AROT_FUSED 0  // 1: fused transposes take part too (A/B knob)
+#endif
 #ifndef BM_TR_AROT_FORCE
 #define BM_TR_AROT_FORCE 0  // 1: always the staggered order, no tuner (A/B knob)
 #endif
@@ -1170,7 +1173,8 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     return BM_OK;
   }
   hipEvent_t t0 = nullptr, t1 = nullptr;
-  if (BM_TR_AROT && !fused && ntB > 1 && ntA >= ntB * BM_TR_AROT && loop_n == 1 && !td.xcd8) {
+  if (BM_TR_AROT && (!fused || BM_TR_AROT_FUSED) && ntB > 1 && ntA >= ntB * BM_TR_AROT && loop_n == 1 &&
+      !td.xcd8) {
     // the two orders to choose from per source buffer (OrderTuner)
     uint64_t sig = 1469598103934665603ull;
     for (uint64_t x : {ntA, ntB, nb, (uint64_t)TA, (uint64_t)TB, (uint64_t)es, (uint64_t)td.sb, (uint64_t)td.da})

@@ -386,3 +386,28 @@ def test_adaptive_transpose_order(shape, perm, dtype):
     summ = (ctypes.c_int64 * 3)()
     assert lib.bm_tune_summary(summ) == 0
     assert summ[0] == 1 and summ[1] == 1, list(summ)
+
+
+def test_adaptive_order_many_buffers():
+    """More source buffers than the tuner keeps (64): the least recently used
+    entries are evicted (their events released) and every output stays exact."""
+    import ctypes
+    import torch
+    from bolt_amd.mi355x import _lib
+    lib = _lib.load()
+    assert lib.bm_tune_reset() == 0
+    be = _be()
+    shape, perm = (300, 512), (1, 0)
+    xs = [_rand(shape, np.float32, 100 + i) for i in range(70)]
+    srcs = [_dev(x) for x in xs]
+    for rep in range(4):
+        for x, src in zip(xs, srcs):
+            out = torch.empty_like(src)
+            be.permute(src, shape, perm, 4, out)
+            torch.cuda.synchronize()
+            assert _host(out, np.float32, (512, 300)).tobytes() == np.ascontiguousarray(x.T).tobytes()
+    summ = (ctypes.c_int64 * 3)()
+    assert lib.bm_tune_summary(summ) == 0
+    assert summ[0] == 64, list(summ)
+    assert lib.bm_tune_reset() == 0
+    assert lib.bm_tune_summary(summ) == 0 and summ[0] == 0
