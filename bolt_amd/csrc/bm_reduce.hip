@@ -41,6 +41,12 @@ constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: gr
 #ifndef BM_COLS_BLOCKS
 #define BM_COLS_BLOCKS 2048  // split R over blocks below this many column tiles (A/B knob)
 #endif
+#ifndef BM_COLS_TCV
+#define BM_COLS_TCV 256  // column vectors per block at most; the rest of the 256 lanes are row phases (A/B knob)
+#endif
+#ifndef BM_COLS_TCV_MIN
+#define BM_COLS_TCV_MIN 64  // narrowest tile taken to reach BM_COLS_BLOCKS before chunking R (A/B knob)
+#endif
 constexpr int kColsUnroll = BM_COLS_UNROLL;
 #ifndef BM_ROWS_UNROLL
 #define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
@@ -1171,7 +1177,12 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
     p.vec = vec;
     const int64_t ncolv = cdiv(I, vec);
     int tcv = 1;
-    while (tcv < 256 && tcv < ncolv) tcv <<= 1;
+    while (tcv < BM_COLS_TCV && tcv < ncolv) tcv <<= 1;
+    // narrower column tiles (more row phases merged in LDS) before splitting
+    // R into chunks that need a workspace and a combine launch: C4's uint16
+    // var over axis 0 3.50 -> 3.17 ms with 64-vector tiles and no chunks
+    // (profiles/r03zb_ab_tcv.log); the float C2 column statistics move +-2%
+    while (tcv > BM_COLS_TCV_MIN && O * cdiv(ncolv, tcv) < BM_COLS_BLOCKS) tcv >>= 1;
     p.tcv = tcv;
     p.nph = 256 / tcv;
     p.ntc = cdiv(ncolv, tcv);
