@@ -223,6 +223,57 @@ __global__ void __launch_bounds__(kCThreads)
   }
 }
 
+// Record scatter: source records are read front to back, VEC elements per
+// lane, and every element p of record r goes to
+//     dst[(r / group) * gstride + map_a[p] + (r % group) * map_b[p]]
+// (map_a[p] < 0: dropped).  For the packed -> packed moves whose source record
+// is read whole and whose destination runs are chunk boxes: keys_to_values of
+// the trailing keys (group = their extent, map_b = box sizes), values_to_keys
+// and unchunk (group 1).  Reads are one contiguous stream; writes are
+// contiguous runs of whole boxes, adjacent across consecutive records.
+template <int ES, int VEC>
+__global__ void __launch_bounds__(kCThreads)
+    k_recmap_scatter(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ ma,
+                     const int32_t *__restrict__ mb, uint64_t total, FastDiv fvpr, FastDiv fgroup,
+                     int64_t gstride) {
+  typedef typename VecB<ES * VEC>::t V;
+  const uint64_t step = (uint64_t)gridDim.x * kCThreads;
+  for (uint64_t i = (uint64_t)blockIdx.x * kCThreads + threadIdx.x; i < total; i += step) {
+    const uint64_t r = fd_div(i, fvpr);
+    const int64_t p = (int64_t)(i - r * fvpr.d) * VEC;
+    const int32_t a = ma[p];
+    if (a < 0) continue;
+    const uint64_t hi = fd_div(r, fgroup);
+    int64_t d = (int64_t)hi * gstride + a;
+    if (mb) d += (int64_t)(r - hi * fgroup.d) * mb[p];
+    const V x = ld_src(reinterpret_cast<const V *>(src) + i);
+    st_dst(x, reinterpret_cast<V *>(dst + d * ES));
+  }
+}
+
+template <int ES>
+void launch_scatter(const char *src, char *dst, const int32_t *ma, const int32_t *mb, int64_t nrec,
+                    int64_t src_rec, int64_t group, int64_t gstride, int vec, hipStream_t st) {
+  const uint64_t vpr = (uint64_t)(src_rec / vec);
+  const uint64_t total = (uint64_t)nrec * vpr;
+  uint64_t g = (total + kCThreads - 1) / kCThreads;
+  if (g > 16777215ull) g = 16777215ull;  // HIP launch limit, then grid-stride
+  const FastDiv fv = make_fastdiv(vpr), fg = make_fastdiv((uint64_t)group);
+  constexpr int V16 = 16 / ES;
+  if (vec == V16)
+    k_recmap_scatter<ES, V16><<<(int)g, kCThreads, 0, st>>>(src, dst, ma, mb, total, fv, fg, gstride);
+  else if (ES <= 4 && vec == (8 / ES > 0 ? 8 / ES : 1))
+    k_recmap_scatter<ES, (8 / ES > 0 ? 8 / ES : 1)><<<(int)g, kCThreads, 0, st>>>(src, dst, ma, mb, total, fv, fg,
+                                                                                gstride);
+  else if (ES <= 2 && vec == (4 / ES > 0 ? 4 / ES : 1))
+    k_recmap_scatter<ES, (4 / ES > 0 ? 4 / ES : 1)><<<(int)g, kCThreads, 0, st>>>(src, dst, ma, mb, total, fv, fg,
+                                                                                gstride);
+  else if (ES == 1 && vec == 2)
+    k_recmap_scatter<ES, 2><<<(int)g, kCThreads, 0, st>>>(src, dst, ma, mb, total, fv, fg, gstride);
+  else
+    k_recmap_scatter<ES, 1><<<(int)g, kCThreads, 0, st>>>(src, dst, ma, mb, total, fv, fg, gstride);
+}
+
 struct Launch {
   const char *src;
   char *dst;
@@ -363,6 +414,44 @@ extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int6
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     bm_set_error("bm_record_gather: launch failed: %s", hipGetErrorString(e));
+    return BM_E_HIP;
+  }
+  return BM_OK;
+}
+
+extern "C" int bm_record_scatter(const void *src_, void *dst_, int64_t nrec, int64_t src_rec, int64_t group,
+                                 int64_t dst_group_stride, const int32_t *map_a, const int32_t *map_b, int vec,
+                                 int elem_bytes, void *stream) {
+  const int es = elem_bytes;
+  if (nrec < 0 || src_rec <= 0 || group < 1 || dst_group_stride < 0 || vec < 1 || (vec & (vec - 1)) ||
+      (es != 1 && es != 2 && es != 4 && es != 8) || vec * es > 16 || src_rec % vec || dst_group_stride % vec ||
+      src_rec > 0x7fffffffLL) {
+    bm_set_error("bm_record_scatter: bad arguments (nrec %lld, src_rec %lld, group %lld, stride %lld, vec %d, "
+                 "elem_bytes %d)", (long long)nrec, (long long)src_rec, (long long)group,
+                 (long long)dst_group_stride, vec, es);
+    return BM_E_ARG;
+  }
+  if (nrec == 0) return BM_OK;
+  if (!src_ || !dst_ || !map_a) {
+    bm_set_error("bm_record_scatter: null pointer");
+    return BM_E_ARG;
+  }
+  if ((uintptr_t)src_ % (uintptr_t)(vec * es) || (uintptr_t)dst_ % (uintptr_t)(vec * es)) {
+    bm_set_error("bm_record_scatter: buffers not aligned to %d-element vectors", vec);
+    return BM_E_ARG;
+  }
+  const char *src = static_cast<const char *>(src_);
+  char *dst = static_cast<char *>(dst_);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (es) {
+    case 1: launch_scatter<1>(src, dst, map_a, map_b, nrec, src_rec, group, dst_group_stride, vec, st); break;
+    case 2: launch_scatter<2>(src, dst, map_a, map_b, nrec, src_rec, group, dst_group_stride, vec, st); break;
+    case 4: launch_scatter<4>(src, dst, map_a, map_b, nrec, src_rec, group, dst_group_stride, vec, st); break;
+    default: launch_scatter<8>(src, dst, map_a, map_b, nrec, src_rec, group, dst_group_stride, vec, st); break;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    bm_set_error("bm_record_scatter: launch failed: %s", hipGetErrorString(e));
     return BM_E_HIP;
   }
   return BM_OK;

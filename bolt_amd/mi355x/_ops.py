@@ -175,6 +175,29 @@ class HipBackend(object):
                                              int(src_rec), int(dst_rec), ctypes.c_void_p(dmap.data_ptr()),
                                              nparts, parts, int(es), self._stream(src)), "bm_record_gather")
 
+    def record_scatter(self, src, src_off, dst, dst_off, nrec, src_rec, group, gstride, plan, key, es):
+        """dst[(r//group)*gstride + map_a[p] + (r%group)*map_b[p]] = src[r*src_rec + p]
+        (elements; offsets in bytes).  plan = (map_a, map_b, vec) on the host,
+        uploaded once per (device, key) and kept resident."""
+        import torch
+        ck = (src.device, key)
+        hit = self._maps.get(ck)
+        if hit is None:
+            map_a, map_b, vec = plan
+            if map_a.size != src_rec or map_b.size != src_rec:
+                raise ValueError("scatter maps do not match the record size")
+            da = torch.from_numpy(np.ascontiguousarray(map_a, dtype=np.int32)).to(src.device)
+            db = (torch.from_numpy(np.ascontiguousarray(map_b, dtype=np.int32)).to(src.device)
+                  if group > 1 else None)
+            hit = (da, db, int(vec))
+            self._maps[ck] = hit
+        da, db, vec = hit
+        _lib.check(self.lib.bm_record_scatter(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
+                                              int(src_rec), int(group), int(gstride),
+                                              ctypes.c_void_p(da.data_ptr()),
+                                              ctypes.c_void_p(db.data_ptr()) if db is not None else None,
+                                              vec, int(es), self._stream(src)), "bm_record_scatter")
+
     def _workspace(self, stat, code, O, R, I, device):
         import torch
         key = (stat, code, O, R, I)

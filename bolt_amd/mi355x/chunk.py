@@ -19,7 +19,7 @@ import numpy as np
 from bolt_amd.mi355x.context import local_shape
 from bolt_amd.mi355x.dist import permute_sharded, _empty
 from bolt_amd.mi355x.plan import (ChunkGeometry, getplan, check_plan, getnumber, getslices, getmask,
-                                  removepad_slices, k2v_copies, v2k_copies, copies_to_map)
+                                  removepad_slices, k2v_copies, v2k_copies, copies_to_map, copies_to_scatter)
 
 
 RECORD_MAP_MAX_BYTES = 65536  # a source record staged whole in LDS (bm_record_gather)
@@ -28,6 +28,36 @@ RECORD_MAP_MAX_BYTES = 65536  # a source record staged whole in LDS (bm_record_g
 def _fused_rechunk():
     """keys_to_values / values_to_keys packed -> packed (A/B knob BOLT_AMD_FUSED_RECHUNK=0)."""
     return os.environ.get("BOLT_AMD_FUSED_RECHUNK", "1") != "0"
+
+
+def _use_scatter():
+    """unchunk / keys_to_values / values_to_keys of small records as one
+    record scatter (bm_record_scatter; A/B knob BOLT_AMD_SCATTER=0, tests
+    BOLT_AMD_SCATTER=force: also where its writes would be piecewise)."""
+    return os.environ.get("BOLT_AMD_SCATTER", "1") != "0"
+
+
+_SCATTER_PLANS = {}
+
+
+def _scatter_plan(key, build, src_rec, gstride, es):
+    """(map_a, map_b, vec) for a record scatter, or None when the move is not
+    a record scatter or would write lines piecewise (plan.scatter_runs_ok);
+    built once per key (geometry, move, element size)."""
+    from bolt_amd.mi355x.plan import scatter_vec, scatter_runs_ok
+    key = key + (os.environ.get("BOLT_AMD_SCATTER"),)
+    if key in _SCATTER_PLANS:
+        return _SCATTER_PLANS[key]
+    maps = build()
+    plan = None
+    force = os.environ.get("BOLT_AMD_SCATTER") == "force"
+    if maps is not None and (force or scatter_runs_ok(maps[0], maps[1], es)):
+        map_a, map_b = maps
+        plan = (map_a, map_b, scatter_vec(map_a, map_b, src_rec, gstride, es))
+    if len(_SCATTER_PLANS) > 256:
+        _SCATTER_PLANS.clear()
+    _SCATTER_PLANS[key] = plan
+    return plan
 
 
 def _use_record_map(src_rec, es):
@@ -158,6 +188,17 @@ class ChunkedArrayMI355X(object):
         if self._geom.is_identity():
             return self._packed[:nrec * rec * es]  # same bytes, dense order
         dense = _empty(nrec * rec * es, self._packed.device)
+        g = self._geom
+        if nrec and _use_scatter() and _use_record_map(g.size, es):
+            # one stream over the packed records, cores scattered to their
+            # dense places, halos dropped
+            plan = _scatter_plan(("unpack", es) + g.key(), lambda: copies_to_scatter(
+                [(sh, ps, ds, po, do) for sh, ds, ps, do, po in g.copies(unpack=True)], g.size),
+                g.size, rec, es)
+            if plan is not None:
+                self._backend.record_scatter(self._packed, 0, dense, 0, nrec, g.size, 1, rec, plan,
+                                             ("scatter", "unpack", es) + g.key(), es)
+                return dense
         if nrec:
             be = self._backend
             for (cshape, dstr, pstr, doff, poff) in self._geom.copies(unpack=True):
@@ -243,6 +284,26 @@ class ChunkedArrayMI355X(object):
             # packed -> packed in one pass: no exchange, no dense intermediate
             new = ChunkGeometry(newshape[newsplit:], newplan, newpadding)
             lk = [int(k) for k in local_shape(self._ctx, self._shape)[:self._split]]
+            nmov = int(kmask.sum())
+            es = self._dtype.itemsize
+            kfull = np.array_equal(np.asarray(size).reshape(-1), self.kshape[kmask])
+            if (_use_scatter() and kfull and kmask[self._split - nmov:].all() and
+                    _use_record_map(self._geom.size, es) and (self._ctx.world_size == 1 or nmov < self._split)):
+                # the moved keys are the trailing ones, unchunked: every run of
+                # K = their extent old records becomes one new record, old
+                # chunk boxes stacked -- one record scatter
+                K = int(np.prod(self.kshape[kmask], dtype=np.int64))
+                ones = [1] * (self._split - nmov) + [int(k) for k in self.kshape[kmask]]
+                g = self._geom
+                plan = _scatter_plan(("k2v", es, K) + g.key() + new.key(), lambda: copies_to_scatter(
+                    k2v_copies(g, new, ones, kmask), K * g.size, group=K, src_rec=g.size), g.size, new.size, es)
+                if plan is not None:
+                    nold = int(np.prod(lk, dtype=np.int64))
+                    packed = _empty(nold // K * new.size * es, self._packed.device)
+                    self._backend.record_scatter(self._packed, 0, packed, 0, nold, g.size, K, new.size, plan,
+                                                 ("scatter", "k2v", es, K) + g.key() + new.key(), es)
+                    return self._constructor(packed, shape=newshape, split=newsplit, dtype=self._dtype,
+                                             plan=newplan, padding=newpadding, ordered=True, context=self._ctx)
             copies = k2v_copies(self._geom, new, lk, kmask)
             return self._repack(copies, None, newshape, newsplit, newplan, newpadding, new)
         dense = self._unpack()
@@ -271,6 +332,20 @@ class ChunkedArrayMI355X(object):
             new = ChunkGeometry(newshape[newsplit:], newplan, newpadding)
             lk = [int(k) for k in local_shape(self._ctx, self._shape)[:self._split]]
             m = int(np.prod(self.vshape[vmask], dtype=np.int64))
+            es = self._dtype.itemsize
+            if _use_scatter() and _use_record_map(self._geom.size, es) and m * new.size < 2 ** 31:
+                # every old record yields m consecutive new records: one record
+                # scatter, the old packed record read front to back
+                g = self._geom
+                plan = _scatter_plan(("v2k", es, vmask.tobytes()) + g.key() + new.key(), lambda: copies_to_scatter(
+                    v2k_copies(g, new, [], vmask), g.size), g.size, m * new.size, es)
+                if plan is not None:
+                    nold = int(np.prod(lk, dtype=np.int64))
+                    packed = _empty(nold * m * new.size * es, self._packed.device)
+                    self._backend.record_scatter(self._packed, 0, packed, 0, nold, g.size, 1, m * new.size, plan,
+                                                 ("scatter", "v2k", es, vmask.tobytes()) + g.key() + new.key(), es)
+                    return self._constructor(packed, shape=newshape, split=newsplit, dtype=self._dtype,
+                                             plan=newplan, padding=newpadding, ordered=True, context=self._ctx)
             if _use_record_map(self._geom.size, self._dtype.itemsize) and m * new.size < 2 ** 31:
                 # every old record yields m consecutive new records: one record-map
                 # gather with the old packed record staged in LDS

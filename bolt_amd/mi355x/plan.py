@@ -338,6 +338,94 @@ def copies_to_map(copies, dst_len):
     return m.astype(np.int32)
 
 
+def copies_to_scatter(copies, src_len, group=1, src_rec=None):
+    """Strided copies over ``group`` consecutive source records (src_rec
+    elements each, src_len = group * src_rec) -> a scatter plan
+    (map_a, map_b) with
+
+        dst(r_lo, p) = map_a[p] + r_lo * map_b[p]      (p < src_rec, r_lo < group)
+
+    and map_a[p] = -1 where no copy reads element p (halos dropped by an
+    unpack or a values_to_keys).  Returns None when the destinations are not
+    affine in r_lo, or when an element is read more than once."""
+    src_rec = src_len if src_rec is None else src_rec
+    d = np.full(src_len, -1, dtype=np.int64)
+    seen = np.zeros(src_len, dtype=np.int64)
+    for shape, ss, ds, so, do in copies:
+        si = np.full((), so, dtype=np.int64)
+        di = np.full((), do, dtype=np.int64)
+        for n, a, b in zip(shape, ss, ds):
+            ax = np.arange(n, dtype=np.int64)
+            si = np.add.outer(si, ax * a)
+            di = np.add.outer(di, ax * b)
+        si, di = si.reshape(-1), di.reshape(-1)
+        if si.size and (si.min() < 0 or si.max() >= src_len):
+            return None
+        np.add.at(seen, si, 1)
+        d[si] = di
+    if (seen > 1).any():
+        return None
+    d = d.reshape(group, src_rec)
+    used = d[0] >= 0
+    if not (np.array_equal(d >= 0, np.broadcast_to(used, d.shape))):
+        return None
+    map_a = d[0].copy()
+    map_b = np.zeros(src_rec, dtype=np.int64)
+    if group > 1:
+        map_b[used] = d[1, used] - d[0, used]
+        want = map_a[None, :] + np.arange(group, dtype=np.int64)[:, None] * map_b[None, :]
+        if not np.array_equal(d[:, used], want[:, used]):
+            return None
+    if map_a.max(initial=0) >= 2 ** 31 or (map_a[used] + (group - 1) * map_b[used]).max(initial=0) >= 2 ** 31:
+        return None
+    return map_a.astype(np.int32), map_b.astype(np.int32)
+
+
+def scatter_vec(map_a, map_b, src_rec, gstride, es):
+    """Elements per vector of a scatter plan: the widest v (v * es <= 16)
+    such that every aligned group of v source elements is either wholly
+    dropped or lands on v consecutive, v-aligned destinations with one r_lo
+    step (map_b)."""
+    v = max(1, 16 // es)
+    while v > 1:
+        if src_rec % v == 0 and gstride % v == 0:
+            a = map_a.reshape(-1, v).astype(np.int64)
+            b = map_b.reshape(-1, v).astype(np.int64)
+            drop = a[:, 0] < 0
+            ok = np.all((a < 0) == drop[:, None])
+            keep = ~drop
+            if ok and keep.any():
+                ak, bk = a[keep], b[keep]
+                ok = (np.all(ak == ak[:, :1] + np.arange(v)) and np.all(bk == bk[:, :1]) and
+                      np.all(ak[:, 0] % v == 0) and np.all(bk[:, 0] % v == 0))
+            if ok:
+                return v
+        v //= 2
+    return 1
+
+
+def scatter_runs_ok(map_a, map_b, es):
+    """Whether a record scatter writes whole lines: its destination runs
+    (consecutive kept elements landing consecutively) are all 128-B aligned
+    multiples of 128 B, or 1 KiB long on average.  Short misaligned runs leave
+    lines written piecewise by different waves: C5's values_to_keys as a
+    scatter (144-160-B runs) ran 6.7-7.7 ms against 3.9-4.3 ms for the
+    gather (profiles/r03zd_ab_scatter_c5.log)."""
+    a = np.asarray(map_a, dtype=np.int64)
+    b = np.asarray(map_b, dtype=np.int64)
+    keep = a >= 0
+    if not keep.any():
+        return True
+    cont = np.zeros(a.size, dtype=bool)
+    cont[1:] = keep[1:] & keep[:-1] & (a[1:] == a[:-1] + 1) & (b[1:] == b[:-1])
+    first = keep & ~cont
+    starts = np.flatnonzero(first)
+    lens = np.bincount((np.cumsum(first) - 1)[keep], minlength=starts.size)
+    if np.mean(lens) * es >= 1024:
+        return True
+    return bool(np.all((a[starts] * es) % 128 == 0) and np.all((lens * es) % 128 == 0))
+
+
 def _cstrides(shape):
     st = [1] * len(shape)
     for k in range(len(shape) - 2, -1, -1):

@@ -194,6 +194,26 @@ int bm_record_gather(const void *src, void *dst, int64_t nrec, int64_t src_rec,
  * O(32 eps) whatever the offset or outliers of the data.
  * Population variance (M2/n), std = sqrt(var), as statcounter.py:119-130.
  */
+/*
+ * bm_record_scatter -- the packed -> packed moves whose source record is read
+ * whole, as one stream: for record r < nrec (src_rec elements each, records
+ * contiguous) and element p,
+ *     dst[(r / group) * dst_group_stride + map_a[p] + (r % group) * map_b[p]]
+ *         = src[r * src_rec + p]                    (map_a[p] < 0: dropped)
+ * map_a / map_b: DEVICE int32 arrays of src_rec entries (map_b may be NULL:
+ * 0).  Replaces, for small records,
+ *   - keys_to_values of the trailing keys (group = their extent, map_b = the
+ *     chunk box sizes)                     bolt/spark/chunk.py:202-289
+ *   - values_to_keys (group 1)             bolt/spark/chunk.py:291-347
+ *   - unchunk, padding dropped (group 1)   bolt/spark/chunk.py:146-200
+ * vec: elements per vector (power of two, vec * elem_bytes <= 16); the caller
+ * guarantees every aligned vec-group of source elements is dropped whole or
+ * lands on vec consecutive, vec-aligned destinations.  Bit-exact.
+ */
+int bm_record_scatter(const void *src, void *dst, int64_t nrec, int64_t src_rec,
+                      int64_t group, int64_t dst_group_stride, const int32_t *map_a,
+                      const int32_t *map_b, int vec, int elem_bytes, void *stream);
+
 int bm_reduce_workspace_bytes(int stat, int in_dtype, int64_t O, int64_t R,
                               int64_t I, size_t *bytes);
 

@@ -74,6 +74,24 @@ class CpuBackend(object):
         d = _np(dst)[dst_off:dst_off + nrec * dst_rec * es].view(dt).reshape(nrec, dst_rec)
         d[...] = s[:, rmap]
 
+    def record_scatter(self, src, src_off, dst, dst_off, nrec, src_rec, group, gstride, plan, key, es):
+        if nrec == 0:
+            return
+        map_a, map_b, vec = plan
+        map_a = np.asarray(map_a, dtype=np.int64)
+        map_b = np.asarray(map_b, dtype=np.int64)
+        assert map_a.size == src_rec and map_b.size == src_rec and src_rec % vec == 0 and gstride % vec == 0
+        dt = np.dtype((np.void, es))
+        s = _np(src)[src_off:src_off + nrec * src_rec * es].view(dt).reshape(nrec, src_rec)
+        d = _np(dst)[dst_off:].view(dt) if (len(_np(dst)) - dst_off) % es == 0 else None
+        if d is None:
+            d = _np(dst)[dst_off:dst_off + (len(_np(dst)) - dst_off) // es * es].view(dt)
+        keep = map_a >= 0
+        r = np.arange(nrec, dtype=np.int64)[:, None]
+        idx = (r // group) * gstride + map_a[None, keep] + (r % group) * map_b[None, keep]
+        assert idx.min(initial=0) >= 0 and idx.max(initial=-1) < d.size
+        d[idx.reshape(-1)] = s[:, keep].reshape(-1)
+
     def permute(self, src, shape, perm, es, dst):
         a = _np(src).view(np.dtype((np.void, es))).reshape(tuple(shape))
         out = _np(dst).view(np.dtype((np.void, es)))

@@ -165,3 +165,34 @@ def test_identity_chunk_shares_bytes(bctx):
     padded = b.chunk((3, 4), padding=(1, 0))
     assert padded._packed.data_ptr() != b._data.data_ptr()
     assert padded.unchunk().toarray().tobytes() == x.tobytes()
+
+
+SCATTER_CASES = [
+    # (shape, split, dtype, plan, padding): unchunk / k2v of the trailing key /
+    # v2k through the record scatter, against the strided-copy / gather paths
+    ((3, 4, 12, 10), 2, np.float64, (4, 5), (1, 2)),
+    ((2, 5, 9, 8), 2, np.float32, (3, 4), (1, 0)),
+    ((4, 3, 16, 16), 2, np.int16, (8, 8), (2, 2)),
+    ((2, 3, 7, 6), 2, np.uint8, (7, 3), (0, 1)),
+    ((3, 2, 10, 12), 2, np.complex64, (5, 4), (0, 1)),
+]
+
+
+@pytest.mark.parametrize("shape,split,dtype,plan,pad", SCATTER_CASES)
+def test_record_scatter_paths_match(bctx, monkeypatch, shape, split, dtype, plan, pad):
+    """unchunk, keys_to_values of the trailing key and values_to_keys give the
+    same bytes through bm_record_scatter (forced, even where its writes would
+    be piecewise) as through the strided copies / record gather."""
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 200, size=shape).astype(dtype)
+    out = {}
+    for mode in ("0", "force"):
+        monkeypatch.setenv("BOLT_AMD_SCATTER", mode)
+        c = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad)
+        k2v = c.keys_to_values((split - 1,))
+        v2k = c.values_to_keys((0,))
+        out[mode] = [c.unchunk().toarray().tobytes(), k2v._packed.cpu().numpy().tobytes(),
+                     v2k._packed.cpu().numpy().tobytes(), k2v.unchunk().toarray().tobytes(),
+                     v2k.unchunk().toarray().tobytes()]
+    assert out["0"] == out["force"]
+    assert out["force"][0] == x.tobytes()

@@ -31,6 +31,10 @@ def load(path):
     lib.bm_record_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, I64P, ctypes.c_int,
                                      ctypes.c_void_p]
+    if hasattr(lib, "bm_record_scatter"):
+        lib.bm_record_scatter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.bm_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -143,6 +147,70 @@ class RecGather(object):
         return True
 
 
+class RecScatter(object):
+    """C5's unchunk, keys_to_values((2,)) or values_to_keys((0,)) of the
+    (16,16) padding-2 chunking as one bm_record_scatter (chunk.py's plan)."""
+
+    def __init__(self, kind):
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bolt_amd.mi355x import plan
+        g = plan.ChunkGeometry((64, 64), (16, 16), (2, 2))
+        self.nrec, self.src_rec, self.group = 64 ** 3, g.size, 1
+        if kind == "unchunk":
+            maps = plan.copies_to_scatter([(sh, ps, ds, po, do) for sh, ds, ps, do, po in g.copies(unpack=True)],
+                                          g.size)
+            self.gstride = 64 * 64
+        elif kind == "k2v":
+            new = plan.ChunkGeometry((64, 64, 64), (64, 16, 16), (0, 2, 2))
+            self.group = 64
+            maps = plan.copies_to_scatter(plan.k2v_copies(g, new, [1, 1, 64], np.array([False, False, True])),
+                                          64 * g.size, group=64, src_rec=g.size)
+            self.gstride = new.size
+        else:
+            new = plan.ChunkGeometry((64,), (16,), (2,))
+            maps = plan.copies_to_scatter(plan.v2k_copies(g, new, [], np.array([True, False])), g.size)
+            self.gstride = 64 * new.size
+        map_a, map_b = maps
+        self.vec = plan.scatter_vec(map_a, map_b, g.size, self.gstride, 8)
+        self.ma = torch.from_numpy(map_a).cuda()
+        self.mb = torch.from_numpy(map_b).cuda()
+        self.src = torch.randint(0, 255, (self.nrec * g.size * 8,), dtype=torch.uint8, device="cuda")
+        ndst = self.nrec // self.group * self.gstride
+        self.dst = torch.empty(ndst * 8, dtype=torch.uint8, device="cuda")
+        self.bytes = self.src.numel() + self.dst.numel()
+
+    def __call__(self, lib):
+        rc = lib.bm_record_scatter(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
+                                   self.nrec, self.src_rec, self.group, self.gstride,
+                                   ctypes.c_void_p(self.ma.data_ptr()),
+                                   ctypes.c_void_p(self.mb.data_ptr()) if self.group > 1 else None,
+                                   self.vec, 8, stream())
+        assert rc == 0, lib.bm_last_error()
+
+
+class Unchunk(object):
+    """C5's unchunk as the strided copies of the chunk geometry (one per run combination)."""
+
+    def __init__(self):
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bolt_amd.mi355x import plan
+        g = plan.ChunkGeometry((64, 64), (16, 16), (2, 2))
+        nrec = 64 ** 3
+        self.src = torch.randint(0, 255, (nrec * g.size * 8,), dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty(nrec * 4096 * 8, dtype=torch.uint8, device="cuda")
+        self.bytes = self.src.numel() + self.dst.numel()
+        self.args = [(ctypes.c_void_p(self.src.data_ptr() + po * 8), ctypes.c_void_p(self.dst.data_ptr() + do * 8),
+                      len(sh) + 1, i64([nrec] + sh), i64([g.size] + ps), i64([4096] + ds))
+                     for sh, ds, ps, do, po in g.copies(unpack=True)]
+
+    def __call__(self, lib):
+        for a in self.args:
+            rc = lib.bm_copy_strided(*a, 8, stream())
+            assert rc == 0, lib.bm_last_error()
+
+
 class K2V(object):
     """C5's chunked keys_to_values((2,)) as the strided copies chunk.py runs
     (plan.k2v_copies, packed -> packed: 3200-B rows of old chunk boxes)."""
@@ -168,6 +236,10 @@ class K2V(object):
 
 OPS = {
     "c5_k2v": lambda: K2V(),
+    "c5_k2v_scatter": lambda: RecScatter("k2v"),
+    "c5_v2k_scatter": lambda: RecScatter("v2k"),
+    "c5_unchunk": lambda: Unchunk(),
+    "c5_unchunk_scatter": lambda: RecScatter("unchunk"),
     "c5_pack": lambda: RecGather("pack"),
     "c5_pack_whole": lambda: RecGather("pack", True),
     "c5_v2k": lambda: RecGather("v2k"),
