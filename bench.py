@@ -392,6 +392,21 @@ def spark_local8_baseline(x, dtype, workers=8):
                                       t["mean"], t["std"])}
 
 
+def _stdout_to_stderr(fn):
+    """Run fn with file descriptor 1 pointed at 2: the process group's
+    transports print connection chatter on stdout ("[Gloo] Rank 0 is connected
+    to 7 peer ranks ..."), and stdout must carry only the one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     args = parse()
     import torch
@@ -413,17 +428,19 @@ def main():
             # as the group's device backend: no device_id, no eager torch RCCL
             # communicator -- the one RCCL communicator per rank is the
             # library's (MI355XContext, bm_comm_init through the group's store)
-            dist.init_process_group("cpu:gloo,cuda:nccl")
+            _stdout_to_stderr(lambda: dist.init_process_group("cpu:gloo,cuda:nccl"))
         else:
-            dist.init_process_group(backend)
+            _stdout_to_stderr(lambda: dist.init_process_group(backend))
             sys.path.insert(0, os.path.join(HERE, "tests"))
             import cpu_backend
             cpu_backend.install_host_staged_gpu()
 
     import bolt_amd as bolt
     from bolt_amd import MI355XContext
-    ctx = MI355XContext(device=dev)
+    ctx = _stdout_to_stderr(lambda: MI355XContext(device=dev))
     assert ctx.world_size == world
+    if world > 1:
+        _stdout_to_stderr(dist.barrier)  # (a lazily connecting transport talks here)
 
     def barrier():
         torch.cuda.synchronize()
