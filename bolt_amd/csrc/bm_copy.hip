@@ -95,6 +95,9 @@ constexpr int kThreads = 256;
 #ifndef BM_RC_DIAG_LOG2
 #define BM_RC_DIAG_LOG2 0  // diagonal tile side 2^k (0: by row size, 8x8 up to 1 KiB rows, else 16x16; A/B knob)
 #endif
+#ifndef BM_RC_DIAG_LOG2G
+#define BM_RC_DIAG_LOG2G 0  // tile side along g as log2 (0: square, the c side; A/B knob)
+#endif
 #ifndef BM_RC_DIAG_GFAST
 // rowcopy Diag16 tile order: 1 = the g-tiles (the next-fastest row dim, e.g.
 // C3's k, 128-B source step) vary fastest between consecutive tiles, so the
@@ -171,7 +174,8 @@ constexpr int kUnroll = BM_RC_UNROLL;
 // (tools/skew/rowcopy_skew.hip "diag16").  A bijection inside each tile.
 struct Diag16 {
   int on;
-  int lg;        // log2 of the tile side (3: 8x8, 4: 16x16)
+  int lg;        // log2 of the tile side along c (3: 8, 4: 16)
+  int lgg;       // log2 of the tile side along g (= lg for square tiles)
   FastDiv grp;   // Ng * Nc rows per (outer) group
   FastDiv ntc;   // Nc / 16 tiles along c
   FastDiv ntg;   // Ng / 16 tiles along g
@@ -181,9 +185,9 @@ struct Diag16 {
 __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   const uint64_t outer = fd_div(row, t.grp);
   const uint64_t q = row - outer * t.grp.d;
-  const int L = t.lg;
-  const uint64_t D = 1ull << L;
-  const uint64_t tile = q >> (2 * L), w = q & (D * D - 1);
+  const int L = t.lg, LG = t.lgg;
+  const uint64_t D = 1ull << L, DG = 1ull << LG;
+  const uint64_t tile = q >> (L + LG), w = q & (D * DG - 1);
   uint64_t gt, ct;
   if (BM_RC_DIAG_GFAST) {
     ct = fd_div(tile, t.ntg);
@@ -192,8 +196,9 @@ __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
     gt = fd_div(tile, t.ntc);
     ct = tile - gt * t.ntc.d;
   }
-  const uint64_t j = w >> L, k = w & (D - 1);
-  const uint64_t g = gt * D + k, c = ct * D + ((k + j) & (D - 1));
+  // diagonal j, position k along g: a bijection of the D x DG tile
+  const uint64_t j = w >> LG, k = w & (DG - 1);
+  const uint64_t g = gt * DG + k, c = ct * D + ((k + j) & (D - 1));
   return outer * t.grp.d + g * t.nc + c;
 }
 
@@ -873,14 +878,16 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
       // placements, 1-KiB rows +2%, the 64 GiB target -0.4..-1.8%; on 2-4-KiB
       // rows 16x16 is equal or +1%; 32x32 loses everywhere)
       const int lg = BM_RC_DIAG_LOG2 > 0 ? BM_RC_DIAG_LOG2 : (row_bytes <= 1024 ? 3 : 4);
-      const int64_t D = (int64_t)1 << lg;
-      if (f.n % D == 0 && g.n % D == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
+      const int lgg = BM_RC_DIAG_LOG2G > 0 ? BM_RC_DIAG_LOG2G : lg;
+      const int64_t D = (int64_t)1 << lg, DG = (int64_t)1 << lgg;
+      if (f.n % D == 0 && g.n % DG == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
           std::llabs(g.ss) < std::llabs(f.ss)) {
         dg.on = 1;
         dg.lg = lg;
+        dg.lgg = lgg;
         dg.grp = make_fastdiv((uint64_t)(f.n * g.n));
         dg.ntc = make_fastdiv((uint64_t)(f.n / D));
-        dg.ntg = make_fastdiv((uint64_t)(g.n / D));
+        dg.ntg = make_fastdiv((uint64_t)(g.n / DG));
         dg.nc = (uint64_t)f.n;
       }
     }
