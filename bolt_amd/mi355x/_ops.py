@@ -169,6 +169,8 @@ class HipBackend(object):
             parts = record_parts(rmap, int(src_rec), int(es))
             hit = (torch.from_numpy(rmap).to(src.device), len(parts) // 4,
                    _lib.i64_array(parts) if parts else None)
+            if len(self._maps) >= 256:  # bounded: maps of at most 64-KiB records each
+                self._maps.clear()
             self._maps[ck] = hit
         dmap, nparts, parts = hit
         _lib.check(self.lib.bm_record_gather(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
@@ -190,6 +192,8 @@ class HipBackend(object):
             db = (torch.from_numpy(np.ascontiguousarray(map_b, dtype=np.int32)).to(src.device)
                   if group > 1 else None)
             hit = (da, db, int(vec))
+            if len(self._maps) >= 256:  # bounded: maps of at most 64-KiB records each
+                self._maps.clear()
             self._maps[ck] = hit
         da, db, vec = hit
         _lib.check(self.lib.bm_record_scatter(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
