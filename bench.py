@@ -366,7 +366,48 @@ def cpu_baseline(cfg, shape, dtype, rows):
                                      "%.2fs + mean %.2fs + std %.2fs" % (u1 - u0, u2 - u1, u3 - u2)}}
     del rs, s, xs
     out["spark_local8"] = spark_local8_baseline(x[:LOCAL8_ROWS], dtype)
+    out["openmp"] = openmp_baseline(x)
     return out
+
+
+def openmp_baseline(x):
+    """The local mode's three calls as OpenMP C on the host cores
+    (oracle/c/local_step.c, a port: SURVEY 8(d)'s optional multi-core line),
+    on the same input; best of two timed runs after one warm-up."""
+    import ctypes
+    path = os.path.join(HERE, "oracle", "c", "liblocal_step.so")
+    if not os.path.exists(path):
+        return {"value": None, "note": "oracle/c/liblocal_step.so not built"}
+    lib = ctypes.CDLL(path)
+    f32p = ctypes.POINTER(ctypes.c_float)
+    for fn in (lib.local_swap, lib.local_mean, lib.local_std):
+        fn.argtypes = [f32p, f32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+    T = x.shape[0]
+    P = int(np.prod(x.shape[1:]))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    xc = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty((P, T), np.float32)
+    m = np.empty(P, np.float32)
+    sd = np.empty(P, np.float32)
+    ptr = lambda a: a.ctypes.data_as(f32p)
+    best = None
+    for it in range(3):
+        t0 = time.perf_counter()
+        lib.local_swap(ptr(xc), ptr(y), T, P, threads)
+        t1 = time.perf_counter()
+        lib.local_mean(ptr(y), ptr(m), T, P, threads)
+        t2 = time.perf_counter()
+        lib.local_std(ptr(y), ptr(sd), T, P, threads)
+        t3 = time.perf_counter()
+        if it and (best is None or t3 - t0 < best[3] - best[0]):
+            best = (t0, t1, t2, t3)
+    t0, t1, t2, t3 = best
+    N = xc.nbytes
+    total = 2 * N + 2 * (N + P * 4)
+    return {"value": round(total / (t3 - t0) / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "oracle/c/local_step.c (OpenMP, the local mode's ascontiguousarray(transpose) + mean + "
+                      "std) on float32 %s: swap %.3fs + mean %.3fs + std %.3fs, best of 2"
+                      % (str(x.shape), t1 - t0, t2 - t1, t3 - t2)}
 
 
 LOCAL8_ROWS = 1000  # time points of the local[8] analogue's sample (~1 GB)
