@@ -220,7 +220,11 @@ class BoltArrayMI355X(BoltArray):
 
     @property
     def _local_shape(self):
-        return local_shape(self._ctx, self._shape)
+        # shape and context never change after construction: computed once
+        ls = self.__dict__.get("_lshape")
+        if ls is None:
+            ls = self.__dict__["_lshape"] = local_shape(self._ctx, self._shape)
+        return ls
 
     # ---------------------------------------------------------- properties
     @property
