@@ -196,3 +196,40 @@ def test_record_scatter_paths_match(bctx, monkeypatch, shape, split, dtype, plan
                      v2k.unchunk().toarray().tobytes()]
     assert out["0"] == out["force"]
     assert out["force"][0] == x.tobytes()
+
+
+def test_scatter_plans_invert_the_gather_maps():
+    """plan.copies_to_scatter on an unpack is the inverse of the pack-side
+    gather map of the cores (every dense element comes from exactly one
+    packed element, halos dropped), scatter_vec's vectors satisfy their
+    contract, and scatter_runs_ok accepts line-aligned runs only."""
+    from bolt_amd.mi355x.plan import (ChunkGeometry, copies_to_scatter, copies_to_map, scatter_vec,
+                                      scatter_runs_ok)
+    rng = np.random.default_rng(11)
+    for _ in range(60):
+        n = int(rng.integers(1, 4))
+        vshape = tuple(int(v) for v in rng.integers(2, 9, n))
+        plan = tuple(int(rng.integers(1, v + 1)) for v in vshape)
+        pad = tuple(int(rng.integers(0, 2)) if p < v and rng.random() < 0.5 else 0 for p, v in zip(plan, vshape))
+        g = ChunkGeometry(vshape, plan, pad)
+        rec = int(np.prod(vshape))
+        sc = copies_to_scatter([(sh, ps, ds, po, do) for sh, ds, ps, do, po in g.copies(unpack=True)], g.size)
+        assert sc is not None
+        map_a, map_b = sc
+        gather = copies_to_map([(sh, ps, ds, po, do) for sh, ds, ps, do, po in g.copies(unpack=True)], rec)
+        keep = map_a >= 0
+        assert keep.sum() == rec and np.array_equal(np.sort(map_a[keep]), np.arange(rec))
+        assert np.array_equal(gather[map_a[keep]], np.flatnonzero(keep))
+        for es in (1, 2, 4, 8):
+            v = scatter_vec(map_a, map_b, g.size, rec, es)
+            assert v * es <= 16 and g.size % v == 0
+            a = map_a.reshape(-1, v)
+            kept = a[:, 0] >= 0
+            assert np.all((a >= 0) == kept[:, None])
+            assert np.all(a[kept] == a[kept][:, :1] + np.arange(v)) and np.all(a[kept][:, 0] % v == 0)
+    # whole 128-B lines (16 float64 per core row) pass, 144-B misaligned runs fail
+    ok = ChunkGeometry((64, 64), (16, 16), (2, 2))
+    m = copies_to_scatter([(sh, ps, ds, po, do) for sh, ds, ps, do, po in ok.copies(unpack=True)], ok.size)
+    assert scatter_runs_ok(m[0], m[1], 8)
+    runs18 = np.concatenate([np.arange(18) + 20 * k for k in range(4)]).astype(np.int32)
+    assert not scatter_runs_ok(runs18, np.zeros(72, np.int32), 8)
