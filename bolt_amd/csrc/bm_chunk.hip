@@ -42,6 +42,9 @@ constexpr int kMaxParts = 8;
 // applied when the tile count is a multiple of 8)
 #define BM_RECMAP_XCDREG 0
 #endif
+#ifndef BM_STAGE_MASK
+#define BM_STAGE_MASK 1  // 0: ignore stage masks, stage whole ranges (A/B knob)
+#endif
 #ifndef BM_RECMAP_GRIDCAP
 #define BM_RECMAP_GRIDCAP 16384  // blocks per launch, then grid-stride over tiles (A/B knob)
 #endif
@@ -91,6 +94,29 @@ __device__ __forceinline__ void stage_lds(L *sl, const L *s, int64_t n) {
     for (int u = 0; u < kStageU; ++u) {
       const int64_t i = i0 + (int64_t)u * kCThreads;
       if (i < n) sl[i] = v[u];
+    }
+  }
+}
+
+// stage_lds over the units a bitmask marks (bit k: the 16-B unit k of the
+// range), skipping the rest: halo rows the gather never reads stay in HBM.
+template <typename L>
+__device__ __forceinline__ void stage_lds_masked(L *sl, const L *s, int64_t n, const uint32_t *m) {
+  constexpr int kLPU = 16 / (int)sizeof(L) > 0 ? 16 / (int)sizeof(L) : 1;  // L-vectors per 16-B unit
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)kStageU * kCThreads) {
+    L v[kStageU];
+    bool use[kStageU];
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int64_t i = i0 + (int64_t)u * kCThreads;
+      const int64_t k = i / kLPU;
+      use[u] = i < n && ((m[k >> 5] >> (k & 31)) & 1u);
+      if (use[u]) v[u] = ld_src(s + i);
+    }
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int64_t i = i0 + (int64_t)u * kCThreads;
+      if (use[u]) sl[i] = v[u];
     }
   }
 }
@@ -161,7 +187,8 @@ __global__ void __launch_bounds__(kCThreads)
 template <int ES, int VEC, int LB>
 __global__ void __launch_bounds__(kCThreads)
     k_recmap_parts(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ map,
-                   Parts P, int64_t src_rec, int64_t dst_rec, int64_t nrec) {
+                   Parts P, int64_t src_rec, int64_t dst_rec, int64_t nrec, const uint32_t *__restrict__ mask,
+                   int mask_words, int64_t mask_off) {
   typedef typename Elem<ES>::t T;
   typedef typename VecB<LB>::t L;
   typedef typename VecB<ES * VEC>::t V;
@@ -169,13 +196,22 @@ __global__ void __launch_bounds__(kCThreads)
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = nrec * P.n;
   const bool reg = BM_RECMAP_XCDREG && ntiles % 8 == 0 && gridDim.x % 8 == 0;
+  uint32_t *lmask = reinterpret_cast<uint32_t *>(smem + mask_off);
+  if (mask) {  // every part's unit mask, once per block
+    for (int i = threadIdx.x; i < P.n * mask_words; i += kCThreads) lmask[i] = mask[i];
+    __syncthreads();
+  }
   for (int64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
     const int64_t t = reg ? (t0 % 8) * (ntiles / 8) + t0 / 8 : t0;
     const int64_t r = t / P.n;
     const int p = (int)(t - r * P.n);
     const int64_t slo = P.slo[p], dlo = P.dlo[p];
-    stage_lds(reinterpret_cast<L *>(smem), reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES),
-              (P.shi[p] - slo) * ES / LB);
+    if (mask)
+      stage_lds_masked(reinterpret_cast<L *>(smem), reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES),
+                       (P.shi[p] - slo) * ES / LB, lmask + p * mask_words);
+    else
+      stage_lds(reinterpret_cast<L *>(smem), reinterpret_cast<const L *>(src + (r * src_rec + slo) * ES),
+                (P.shi[p] - slo) * ES / LB);
     __syncthreads();
     constexpr int GU = GatherU<VEC>::v;
     const int64_t nout = (P.dhi[p] - dlo) / VEC;
@@ -280,6 +316,9 @@ struct Launch {
   const int32_t *map;
   int64_t src_rec, dst_rec, nrec, rb;
   const Parts *parts;  // null: whole records, rb per tile
+  const uint32_t *mask;  // parts only: 16-B unit masks of the staged ranges (null: stage all)
+  int mask_words;
+  int64_t mask_off;
   int grid;
   size_t shmem;
   hipStream_t st;
@@ -289,7 +328,8 @@ template <int ES, int VEC, int LB>
 void launch_one(const Launch &L) {
   if (L.parts)
     k_recmap_parts<ES, VEC, LB><<<L.grid, kCThreads, L.shmem, L.st>>>(L.src, L.dst, L.map, *L.parts, L.src_rec,
-                                                                       L.dst_rec, L.nrec);
+                                                                       L.dst_rec, L.nrec, L.mask, L.mask_words,
+                                                                       L.mask_off);
   else
     k_recmap_lds<ES, VEC, LB><<<L.grid, kCThreads, L.shmem, L.st>>>(L.src, L.dst, L.map, L.src_rec, L.dst_rec,
                                                                      L.nrec, L.rb, make_fastdiv((uint64_t)L.dst_rec));
@@ -324,9 +364,20 @@ int pow2_align(uintptr_t a, int64_t bytes, int cap) {
 
 }  // namespace
 
+extern "C" int bm_record_gather_masked(const void *src_, void *dst_, int64_t nrec, int64_t src_rec,
+                                       int64_t dst_rec, const int32_t *map, int nparts, const int64_t *parts,
+                                       const uint32_t *stage_mask, int mask_words, int elem_bytes, void *stream);
+
 extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int64_t src_rec, int64_t dst_rec,
                                 const int32_t *map, int nparts, const int64_t *parts, int elem_bytes,
                                 void *stream) {
+  return bm_record_gather_masked(src_, dst_, nrec, src_rec, dst_rec, map, nparts, parts, nullptr, 0, elem_bytes,
+                                 stream);
+}
+
+extern "C" int bm_record_gather_masked(const void *src_, void *dst_, int64_t nrec, int64_t src_rec,
+                                       int64_t dst_rec, const int32_t *map, int nparts, const int64_t *parts,
+                                       const uint32_t *stage_mask, int mask_words, int elem_bytes, void *stream) {
   if (nrec < 0 || src_rec <= 0 || dst_rec <= 0 || src_rec > 0x7fffffffLL || nparts < 0 || nparts > kMaxParts ||
       (nparts > 1 && !parts) || (elem_bytes != 1 && elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8)) {
     bm_set_error("bm_record_gather: bad arguments (nrec %lld, src_rec %lld, dst_rec %lld, nparts %d, elem_bytes %d)",
@@ -382,12 +433,29 @@ extern "C" int bm_record_gather(const void *src_, void *dst_, int64_t nrec, int6
       L.rb = 1;
       L.parts = &P;
       L.shmem = (size_t)(span * es + 15) / 16 * 16;
+      L.mask = nullptr;
+      L.mask_words = 0;
+      L.mask_off = (int64_t)L.shmem;
+      if (BM_STAGE_MASK && stage_mask && mask_words > 0) {
+        // one bit per 16-B unit of the widest range (checked against it), all parts' masks in LDS
+        if ((int64_t)mask_words * 32 * 16 < span * es) {
+          bm_set_error("bm_record_gather: %d mask words cannot cover %lld-B ranges", mask_words,
+                       (long long)(span * es));
+          return BM_E_ARG;
+        }
+        L.mask = stage_mask;
+        L.mask_words = mask_words;
+        L.shmem += (size_t)nparts * mask_words * 4;
+      }
       ntiles = nrec * nparts;
     } else {
       int64_t rb = rec_bytes >= kStageBytes ? 1 : kStageBytes / rec_bytes;
       if (rb > nrec) rb = nrec;
       L.rb = rb;
       L.parts = nullptr;
+      L.mask = nullptr;
+      L.mask_words = 0;
+      L.mask_off = 0;
       L.shmem = (size_t)(rb * rec_bytes + 15) / 16 * 16;
       ntiles = (nrec + rb - 1) / rb;
     }

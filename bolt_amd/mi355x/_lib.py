@@ -37,6 +37,9 @@ SIGNATURES = {
                                   _c.c_void_p, _c.c_int64, _c.c_void_p]),
     "bm_record_gather": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,
                                     _c.c_void_p, _c.c_int, _i64p, _c.c_int, _c.c_void_p]),
+    "bm_record_gather_masked": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,
+                                           _c.c_void_p, _c.c_int, _i64p, _c.c_void_p, _c.c_int, _c.c_int,
+                                           _c.c_void_p]),
     "bm_record_scatter": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,
                                      _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_void_p]),
     "bm_reduce_workspace_bytes": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int64, _c.c_int64,

@@ -77,6 +77,31 @@ def record_parts(rmap, src_rec, es, part_bytes=None):
     return []
 
 
+STAGE_MASK_MIN_SKIP = 0.05  # stage masks only when they keep at least this share of units in HBM
+
+
+def stage_mask(rmap, parts, es):
+    """(uint32 mask [nparts x words], words) of the 16-B units of each part's
+    source range [slo, shi) that its map entries read, or (None, 0) when there
+    are no parts or the mask would skip less than STAGE_MASK_MIN_SKIP of the
+    staged units (values_to_keys skips the moved axis' halo rows: ~16% on C5)."""
+    import os
+    if not parts or os.environ.get("BOLT_AMD_STAGE_MASK", "1") == "0":  # A/B knob
+        return None, 0
+    p4 = np.asarray(parts, dtype=np.int64).reshape(-1, 4)
+    units = [(-(-(int(shi - slo) * es) // 16)) for _, _, slo, shi in p4]
+    words = max(1, -(-max(units) // 32))
+    mask = np.zeros((len(p4), words * 32), dtype=bool)
+    for k, (dlo, dhi, slo, shi) in enumerate(p4):
+        mask[k, ((np.asarray(rmap[dlo:dhi], dtype=np.int64) - slo) * es) // 16] = True
+    if 1.0 - mask.sum() / float(sum(units)) < STAGE_MASK_MIN_SKIP:
+        return None, 0
+    # bit j of word w is unit 32 w + j
+    m = mask.reshape(len(p4), words, 32).astype(np.uint64)
+    words32 = (m << np.arange(32, dtype=np.uint64)).sum(axis=2).astype(np.uint32)
+    return np.ascontiguousarray(words32.reshape(-1)), words
+
+
 def raw_stream(device):
     """Handle of torch's current HIP stream on ``device`` (what
     ``torch.cuda.current_stream(device).cuda_stream`` returns, without building
@@ -167,15 +192,19 @@ class HipBackend(object):
             if rmap.size != dst_rec or rmap.min() < 0 or rmap.max() >= src_rec:
                 raise ValueError("record map does not match the record sizes")
             parts = record_parts(rmap, int(src_rec), int(es))
+            mask, words = stage_mask(rmap, parts, int(es))
             hit = (torch.from_numpy(rmap).to(src.device), len(parts) // 4,
-                   _lib.i64_array(parts) if parts else None)
+                   _lib.i64_array(parts) if parts else None,
+                   torch.from_numpy(mask).to(src.device) if mask is not None else None, words)
             if len(self._maps) >= 256:  # bounded: maps of at most 64-KiB records each
                 self._maps.clear()
             self._maps[ck] = hit
-        dmap, nparts, parts = hit
-        _lib.check(self.lib.bm_record_gather(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
-                                             int(src_rec), int(dst_rec), ctypes.c_void_p(dmap.data_ptr()),
-                                             nparts, parts, int(es), self._stream(src)), "bm_record_gather")
+        dmap, nparts, parts, dmask, words = hit
+        _lib.check(self.lib.bm_record_gather_masked(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
+                                                    int(src_rec), int(dst_rec), ctypes.c_void_p(dmap.data_ptr()),
+                                                    nparts, parts,
+                                                    ctypes.c_void_p(dmask.data_ptr()) if dmask is not None else None,
+                                                    words, int(es), self._stream(src)), "bm_record_gather_masked")
 
     def record_scatter(self, src, src_off, dst, dst_off, nrec, src_rec, group, gstride, plan, key, es):
         """dst[(r//group)*gstride + map_a[p] + (r%group)*map_b[p]] = src[r*src_rec + p]

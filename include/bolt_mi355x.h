@@ -195,6 +195,20 @@ int bm_record_gather(const void *src, void *dst, int64_t nrec, int64_t src_rec,
  * Population variance (M2/n), std = sqrt(var), as statcounter.py:119-130.
  */
 /*
+ * bm_record_gather_masked -- bm_record_gather whose (record, part) tiles
+ * stage only the 16-B units of their source range that the map reads:
+ * stage_mask (DEVICE, nparts x mask_words uint32) has bit k of part p set
+ * when unit k (bytes [16k, 16k + 16) from the part's slo) holds an element
+ * the part's map entries name.  values_to_keys drops the moved axis' halo
+ * rows, which then stay in HBM (bolt/spark/chunk.py:291-347, removepad
+ * :514-550).  A NULL mask stages everything (= bm_record_gather).
+ */
+int bm_record_gather_masked(const void *src, void *dst, int64_t nrec, int64_t src_rec,
+                            int64_t dst_rec, const int32_t *map, int nparts,
+                            const int64_t *parts, const uint32_t *stage_mask,
+                            int mask_words, int elem_bytes, void *stream);
+
+/*
  * bm_record_scatter -- the packed -> packed moves whose source record is read
  * whole, as one stream: for record r < nrec (src_rec elements each, records
  * contiguous) and element p,

@@ -35,6 +35,10 @@ def load(path):
         lib.bm_record_scatter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    if hasattr(lib, "bm_record_gather_masked"):
+        lib.bm_record_gather_masked.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, I64P,
+                                                ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     lib.bm_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -109,7 +113,7 @@ class RecGather(object):
     """C5's chunk pack ((16,16), padding 2 on 64x64 float64 records) or its
     values_to_keys((0,)) repack, as one bm_record_gather (parts as _ops picks)."""
 
-    def __init__(self, kind, nparts_off=False, part_bytes=None):
+    def __init__(self, kind, nparts_off=False, part_bytes=None, masked=False):
         import os
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from bolt_amd.mi355x import plan, _ops
@@ -125,15 +129,25 @@ class RecGather(object):
         self.dst_rec = rmap.size
         parts = [] if nparts_off else _ops.record_parts(rmap, self.src_rec, 8, part_bytes)
         self.nparts, self.parts = len(parts) // 4, (i64(parts) if parts else None)
+        self.mask, self.words = None, 0
+        if masked:
+            m, self.words = _ops.stage_mask(rmap, parts, 8)
+            self.mask = torch.from_numpy(m).cuda()
         self.map = torch.from_numpy(rmap).cuda()
         self.src = torch.randint(0, 255, (self.nrec * self.src_rec * 8,), dtype=torch.uint8, device="cuda")
         self.dst = torch.empty(self.nrec * self.dst_rec * 8, dtype=torch.uint8, device="cuda")
         self.bytes = self.src.numel() + self.dst.numel()
 
     def __call__(self, lib):
-        rc = lib.bm_record_gather(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
-                                  self.nrec, self.src_rec, self.dst_rec, ctypes.c_void_p(self.map.data_ptr()),
-                                  self.nparts, self.parts, 8, stream())
+        if self.mask is not None:
+            rc = lib.bm_record_gather_masked(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
+                                             self.nrec, self.src_rec, self.dst_rec,
+                                             ctypes.c_void_p(self.map.data_ptr()), self.nparts, self.parts,
+                                             ctypes.c_void_p(self.mask.data_ptr()), self.words, 8, stream())
+        else:
+            rc = lib.bm_record_gather(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
+                                      self.nrec, self.src_rec, self.dst_rec, ctypes.c_void_p(self.map.data_ptr()),
+                                      self.nparts, self.parts, 8, stream())
         assert rc == 0, lib.bm_last_error()
 
     def check(self):
@@ -244,6 +258,7 @@ OPS = {
     "c5_pack_whole": lambda: RecGather("pack", True),
     "c5_v2k": lambda: RecGather("v2k"),
     "c5_v2k_whole": lambda: RecGather("v2k", True),
+    "c5_v2k_masked": lambda: RecGather("v2k", masked=True),
     "c5_v2k_pb16k": lambda: RecGather("v2k", part_bytes=16 << 10),
     "c5_v2k_pb24k": lambda: RecGather("v2k", part_bytes=24 << 10),
     "c2_copy": lambda: Copy(2097152000),
