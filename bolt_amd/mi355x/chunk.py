@@ -5,12 +5,17 @@ A chunked array's records are ``(key + chunk_id, chunk_value)`` pairs
 HBM, in chunk-id order, each chunk a dense box of its (padded) extent -- the
 layout described by plan.ChunkGeometry.  Building it (pack) and undoing it
 (unpack, padding removed) are strided-copy kernels, one launch per run of
-equally shaped chunks; records never leave their GPU.
+equally shaped chunks, or for records of at most 64 KiB one record-map
+gather (pack) / record scatter (unpack); when the packed layout is the dense
+one both are relabellings.  Records never leave their GPU.
 
 keys_to_values / values_to_keys change which axes are keys and re-chunk the
 moved axes; their result is by construction the chunking of the permuted
-array with the new plan/padding (chunk.py:202-347), so they run as
-unpack -> permute (RCCL all-to-all if the sharded axis moves) -> pack.
+array with the new plan/padding (chunk.py:202-347).  They go packed ->
+packed in one pass where the leading key stays (strided copies, a record
+scatter for trailing keys, a masked record gather for values_to_keys), and
+otherwise unpack -> permute (RCCL all-to-all if the sharded axis moves) ->
+pack.
 """
 import os
 
