@@ -267,23 +267,43 @@ __global__ void __launch_bounds__(kCThreads)
 // the trailing keys (group = their extent, map_b = box sizes), values_to_keys
 // and unchunk (group 1).  Reads are one contiguous stream; writes are
 // contiguous runs of whole boxes, adjacent across consecutive records.
+#ifndef BM_SCATTER_U
+#define BM_SCATTER_U 1  // source vectors per lane per round, all in flight together (A/B knob)
+#endif
+#ifndef BM_SCATTER_SPEC
+#define BM_SCATTER_SPEC 0  // 1: load the source vector before its map entry arrives (A/B knob)
+#endif
 template <int ES, int VEC>
 __global__ void __launch_bounds__(kCThreads)
     k_recmap_scatter(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ ma,
                      const int32_t *__restrict__ mb, uint64_t total, FastDiv fvpr, FastDiv fgroup,
                      int64_t gstride) {
   typedef typename VecB<ES * VEC>::t V;
-  const uint64_t step = (uint64_t)gridDim.x * kCThreads;
-  for (uint64_t i = (uint64_t)blockIdx.x * kCThreads + threadIdx.x; i < total; i += step) {
-    const uint64_t r = fd_div(i, fvpr);
-    const int64_t p = (int64_t)(i - r * fvpr.d) * VEC;
-    const int32_t a = ma[p];
-    if (a < 0) continue;
-    const uint64_t hi = fd_div(r, fgroup);
-    int64_t d = (int64_t)hi * gstride + a;
-    if (mb) d += (int64_t)(r - hi * fgroup.d) * mb[p];
-    const V x = ld_src(reinterpret_cast<const V *>(src) + i);
-    st_dst(x, reinterpret_cast<V *>(dst + d * ES));
+  constexpr int U = BM_SCATTER_U;
+  const uint64_t step = (uint64_t)gridDim.x * kCThreads * U;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kCThreads * U + threadIdx.x; i0 < total; i0 += step) {
+    V x[U];
+    int64_t d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + (uint64_t)u * kCThreads;
+      d[u] = -1;
+      if (i < total) {
+        if (BM_SCATTER_SPEC) x[u] = ld_src(reinterpret_cast<const V *>(src) + i);
+        const uint64_t r = fd_div(i, fvpr);
+        const int64_t p = (int64_t)(i - r * fvpr.d) * VEC;
+        const int32_t a = ma[p];
+        if (a >= 0) {
+          const uint64_t hi = fd_div(r, fgroup);
+          d[u] = (int64_t)hi * gstride + a;
+          if (mb) d[u] += (int64_t)(r - hi * fgroup.d) * mb[p];
+          if (!BM_SCATTER_SPEC) x[u] = ld_src(reinterpret_cast<const V *>(src) + i);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (d[u] >= 0) st_dst(x[u], reinterpret_cast<V *>(dst + d[u] * ES));
   }
 }
 
@@ -292,7 +312,7 @@ void launch_scatter(const char *src, char *dst, const int32_t *ma, const int32_t
                     int64_t src_rec, int64_t group, int64_t gstride, int vec, hipStream_t st) {
   const uint64_t vpr = (uint64_t)(src_rec / vec);
   const uint64_t total = (uint64_t)nrec * vpr;
-  uint64_t g = (total + kCThreads - 1) / kCThreads;
+  uint64_t g = (total + (uint64_t)kCThreads * BM_SCATTER_U - 1) / ((uint64_t)kCThreads * BM_SCATTER_U);
   if (g > 16777215ull) g = 16777215ull;  // HIP launch limit, then grid-stride
   const FastDiv fv = make_fastdiv(vpr), fg = make_fastdiv((uint64_t)group);
   constexpr int V16 = 16 / ES;

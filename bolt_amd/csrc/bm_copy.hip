@@ -25,7 +25,6 @@
 
 #include <algorithm>
 #include <cstdlib>
-#include <mutex>
 #include <vector>
 
 namespace {
@@ -136,8 +135,9 @@ constexpr int kThreads = 256;
 // transpose, staggered order: tile (ta, tb) takes a-tile (ta + tb * ntA /
 // (ntB * BM_TR_AROT)) mod ntA, so the b-tiles in flight together (one per XCD
 // on C2) read their source rows at offsets 1/ntB of a row apart while each
-// keeps a contiguous window.  Whether it runs is decided per source buffer
-// (OrderTuner below); 0 = never.
+// keeps a contiguous window.  It runs only under BM_TR_AROT_FORCE: it was
+// faster on some buffers and slower on others (profiles/r03t_ab_arot*.log),
+// and the round-3 per-buffer tuner never picked it on the driver's box.
 #define BM_TR_AROT 1
 #endif
 #ifndef BM_TR_AROT_DELTA
@@ -147,7 +147,7 @@ constexpr int kThreads = 256;
 #define BM_TR_AROT_FUSED 0  // 1: fused transposes take part too (A/B knob)
 #endif
 #ifndef BM_TR_AROT_FORCE
-#define BM_TR_AROT_FORCE 0  // 1: always the staggered order, no tuner (A/B knob)
+#define BM_TR_AROT_FORCE 0  // 1: the staggered order (A/B knob)
 #endif
 #ifndef BM_TR_LOOP
 #define BM_TR_LOOP 0  // transpose: each block walks the batch dim that is page-local on both sides, if >= this many blocks remain (0 = off; A/B knob)
@@ -723,122 +723,6 @@ int grid_for(uint64_t work_items, uint64_t per_block, uint64_t cap = 256ull * 16
 
 bool aligned(const void *p, int64_t a) { return ((uintptr_t)p % (uintptr_t)a) == 0; }
 
-// ------------------------------------------------ placement-adaptive order --
-// Two tile orders of the unfused transpose write the same bytes, and which one
-// is faster depends on where the source buffer's pages landed physically: on
-// the C2 swap the staggered order (BM_TR_AROT) runs 6-7% faster than the
-// in-order walk on most buffers and 5% slower on others, in one process on one
-// box (profiles/r03t_ab_arot.log, r03t_ab_arot2.log).  A kernel cannot see
-// physical addresses, so the library measures: per (source buffer, copy
-// shape), call 1 runs in order untimed (it may write a fresh destination and
-// pay its first touch), calls 2 and 3 run each order once between hipEvents on
-// the caller's stream, and the first later call that finds both timings
-// complete (hipEventQuery: the host never waits) keeps the faster order for
-// good; until then the in-order walk runs.  BOLT_AMD_ADAPTIVE=0 disables it.
-class OrderTuner {
- public:
-  // Order for this call (0 = in order, 1 = staggered); *t0 / *t1: events to
-  // record before / after the launch (null: untimed).
-  int pick(const void *src, uint64_t sig, hipEvent_t *t0, hipEvent_t *t1) {
-    *t0 = *t1 = nullptr;
-    std::lock_guard<std::mutex> g(mu_);
-    if (enabled_ < 0) {
-      const char *e = std::getenv("BOLT_AMD_ADAPTIVE");
-      enabled_ = (e && e[0] == '0') ? 0 : 1;
-    }
-    if (!enabled_) return 0;
-    Entry &E = find(src, sig);
-    E.stamp = ++clock_;
-    if (E.choice >= 0) return E.choice;
-    ++E.calls;
-    if (E.calls == 1) return 0;
-    if (E.calls <= 3) {
-      const int v = E.calls - 2;
-      for (int k = 0; k < 2; ++k)
-        if (!E.ev[v][k] && hipEventCreate(&E.ev[v][k]) != hipSuccess) {
-          E.ev[v][k] = nullptr;
-          (void)hipGetLastError();
-          E.choice = 0;  // no timing available: stay in order
-          release(E);
-          return 0;
-        }
-      *t0 = E.ev[v][0];
-      *t1 = E.ev[v][1];
-      return v;
-    }
-    const bool done = hipEventQuery(E.ev[0][1]) == hipSuccess && hipEventQuery(E.ev[1][1]) == hipSuccess;
-    (void)hipGetLastError();  // a not-ready query is not an error of this call
-    if (!done) return 0;
-    float ms[2] = {0.f, 0.f};
-    bool ok = true;
-    for (int v = 0; v < 2; ++v) ok = ok && hipEventElapsedTime(&ms[v], E.ev[v][0], E.ev[v][1]) == hipSuccess;
-    (void)hipGetLastError();
-    E.choice = (ok && ms[1] < 0.99f * ms[0]) ? 1 : 0;  // ties keep the in-order walk
-    E.ms[0] = ms[0];
-    E.ms[1] = ms[1];
-    release(E);
-    return E.choice;
-  }
-
-  // entries, decided, decided for the staggered order
-  void summary(int64_t *out) {
-    std::lock_guard<std::mutex> g(mu_);
-    out[0] = (int64_t)v_.size();
-    out[1] = out[2] = 0;
-    for (const Entry &E : v_) {
-      out[1] += E.choice >= 0;
-      out[2] += E.choice == 1;
-    }
-  }
-
-  void reset() {
-    std::lock_guard<std::mutex> g(mu_);
-    for (Entry &E : v_) release(E);
-    v_.clear();
-    enabled_ = -1;
-  }
-
- private:
-  struct Entry {
-    const void *src;
-    uint64_t sig, stamp;
-    int calls, choice;
-    hipEvent_t ev[2][2];
-    float ms[2];
-  };
-  static constexpr size_t kCap = 64;
-
-  Entry &find(const void *src, uint64_t sig) {
-    for (Entry &E : v_)
-      if (E.src == src && E.sig == sig) return E;
-    if (v_.size() >= kCap) {  // evict the least recently used
-      size_t o = 0;
-      for (size_t i = 1; i < v_.size(); ++i)
-        if (v_[i].stamp < v_[o].stamp) o = i;
-      release(v_[o]);
-      v_.erase(v_.begin() + (long)o);
-    }
-    v_.push_back(Entry{src, sig, 0, 0, -1, {{nullptr, nullptr}, {nullptr, nullptr}}, {0.f, 0.f}});
-    return v_.back();
-  }
-
-  static void release(Entry &E) {
-    for (auto &pair : E.ev)
-      for (hipEvent_t &e : pair)
-        if (e) {
-          (void)hipEventDestroy(e);
-          e = nullptr;
-        }
-  }
-
-  std::mutex mu_;
-  std::vector<Entry> v_;
-  uint64_t clock_ = 0;
-  int enabled_ = -1;
-};
-
-OrderTuner g_order_tuner;
-
 int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int es,
                    hipStream_t st) {
   const Dim inner = dims.back();
@@ -1132,7 +1016,7 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   td.asp = make_fastdiv(1);
   td.aspq = ntA;
   td.ntA = ntA;
-  td.arot = 0;  // set per call by the order tuner (unfused k_transpose only)
+  td.arot = 0;  // in-order walk (the staggered order is an A/B knob, below)
   if (BM_TR_ASPREAD > 1 && fused && ntA % BM_TR_ASPREAD == 0 && ntA >= 2 * BM_TR_ASPREAD) {
     td.asp = make_fastdiv(BM_TR_ASPREAD);
     td.aspq = ntA / BM_TR_ASPREAD;
@@ -1179,17 +1063,9 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
                                                                               (uint8_t *)dst, tp);
     return BM_OK;
   }
-  hipEvent_t t0 = nullptr, t1 = nullptr;
-  if (BM_TR_AROT && (!fused || BM_TR_AROT_FUSED) && ntB > 1 && ntA >= ntB * BM_TR_AROT && loop_n == 1 &&
-      !td.xcd8) {
-    // the two orders to choose from per source buffer (OrderTuner)
-    uint64_t sig = 1469598103934665603ull;
-    for (uint64_t x : {ntA, ntB, nb, (uint64_t)TA, (uint64_t)TB, (uint64_t)es, (uint64_t)td.sb, (uint64_t)td.da})
-      sig = (sig ^ x) * 1099511628211ull;
-    if (BM_TR_AROT_FORCE || g_order_tuner.pick(src, sig, &t0, &t1))
-      td.arot = (ntA / (ntB * BM_TR_AROT) + BM_TR_AROT_DELTA) % ntA;
-  }
-  if (t0) (void)hipEventRecord(t0, st);
+  if (BM_TR_AROT_FORCE && BM_TR_AROT && (!fused || BM_TR_AROT_FUSED) && ntB > 1 && ntA >= ntB * BM_TR_AROT &&
+      loop_n == 1 && !td.xcd8)
+    td.arot = (ntA / (ntB * BM_TR_AROT) + BM_TR_AROT_DELTA) % ntA;  // staggered order (A/B knob)
   int rc = BM_E_ARG;
   switch (es) {
     case 1: rc = launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, false, st, loop_n); break;
@@ -1198,7 +1074,6 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     case 8: rc = launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, fused, st, loop_n); break;
     default: bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);
   }
-  if (t1) (void)hipEventRecord(t1, st);
   return rc;
 }
 
@@ -1397,20 +1272,3 @@ extern "C" int bm_permute(const void *src, void *dst, int ndim, const int64_t *s
   return bm_copy_strided(src, dst, ndim, oshape, srcs, dstr, elem_bytes, stream);
 }
 
-// Summary of the placement-adaptive transpose order (OrderTuner): out[0] =
-// (source buffer, shape) entries, out[1] = decided, out[2] = decided for the
-// staggered order.
-extern "C" int bm_tune_summary(int64_t *out) {
-  if (!out) {
-    bm_set_error("bm_tune_summary: null output");
-    return BM_E_ARG;
-  }
-  g_order_tuner.summary(out);
-  return BM_OK;
-}
-
-// Forget every decision and re-read BOLT_AMD_ADAPTIVE (tests).
-extern "C" int bm_tune_reset(void) {
-  g_order_tuner.reset();
-  return BM_OK;
-}

@@ -31,8 +31,6 @@ SIGNATURES = {
                                    _c.c_int, _c.c_void_p]),
     "bm_permute": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int, _i64p,
                               _c.POINTER(_c.c_int32), _c.c_int, _c.c_void_p]),
-    "bm_tune_summary": (_c.c_int, [_i64p]),
-    "bm_tune_reset": (_c.c_int, []),
     "bm_gather_rows": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,
                                   _c.c_void_p, _c.c_int64, _c.c_void_p]),
     "bm_record_gather": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,

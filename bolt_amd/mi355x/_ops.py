@@ -178,6 +178,15 @@ class HipBackend(object):
         # the caching allocator must not hand the index buffer out before the kernel has read it
         didx.record_stream(torch.cuda.current_stream(src.device))
 
+    def _drop_maps(self, device):
+        """Forget the resident maps.  Kernels queued on any stream may still read
+        them, and the caching allocator would hand their blocks out again as
+        soon as the last reference goes: wait for the device first (rare: the
+        cache holds 256 geometries)."""
+        import torch
+        torch.cuda.synchronize(device)
+        self._maps.clear()
+
     def record_gather(self, src, src_off, dst, dst_off, nrec, src_rec, dst_rec, rmap, key, es):
         """dst[r*dst_rec + o] = src[r*src_rec + rmap[o]] (elements; offsets in bytes).
 
@@ -197,7 +206,7 @@ class HipBackend(object):
                    _lib.i64_array(parts) if parts else None,
                    torch.from_numpy(mask).to(src.device) if mask is not None else None, words)
             if len(self._maps) >= 256:  # bounded: maps of at most 64-KiB records each
-                self._maps.clear()
+                self._drop_maps(src.device)
             self._maps[ck] = hit
         dmap, nparts, parts, dmask, words = hit
         _lib.check(self.lib.bm_record_gather_masked(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),
@@ -222,7 +231,7 @@ class HipBackend(object):
                   if group > 1 else None)
             hit = (da, db, int(vec))
             if len(self._maps) >= 256:  # bounded: maps of at most 64-KiB records each
-                self._maps.clear()
+                self._drop_maps(src.device)
             self._maps[ck] = hit
         da, db, vec = hit
         _lib.check(self.lib.bm_record_scatter(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec),

@@ -24,7 +24,7 @@ from bolt_amd.mi355x import _lib
 from bolt_amd.mi355x._ops import backend_for, dtype_code
 from bolt_amd.base import BoltArray
 from bolt_amd.mi355x.context import local_shape
-from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, permute_sharded, redistribute_rows, select_sharded, _empty
+from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, gather_to_host, permute_sharded, redistribute_rows, select_sharded, _empty
 from bolt_amd.mi355x.transfer import finish_host_result, host_result, to_device, to_host
 from bolt_amd.local import BoltArrayLocal
 from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
@@ -942,18 +942,17 @@ class BoltArrayMI355X(BoltArray):
         return self._stat(axis, func=np.minimum, keepdims=keepdims)
 
     # -------------------------------------------------------------- egress
-    def _gathered_bytes(self):
+    def toarray(self):
+        """The whole array on the host (array.py:1006-1014).  Across GPUs the
+        slabs are gathered window by window (dist.gather_to_host): device
+        memory per rank stays at its slab plus one window."""
         ctx = self._ctx
         if ctx.world_size == 1:
-            return self._data
+            return to_host(self._data, self._dtype, self._shape)
         rowbytes = int(np.prod(self._shape[1:], dtype=np.int64)) * self._dtype.itemsize
         rows = self._shape[0] if self._shape else 1  # a 0-d array lives on rank 0
         sizes = [(hi - lo) * rowbytes for lo, hi in ctx.bounds(rows)]
-        return all_gather_bytes(ctx, self._data, sizes)
-
-    def toarray(self):
-        """The whole array on the host (array.py:1006-1014)."""
-        return to_host(self._gathered_bytes(), self._dtype, self._shape)
+        return gather_to_host(ctx, self._data, sizes).view(self._dtype).reshape(self._shape)
 
     def tolocal(self):
         """As a local bolt array (array.py:999-1004)."""

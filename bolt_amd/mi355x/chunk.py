@@ -502,18 +502,13 @@ class ChunkedArrayMI355X(object):
     # ------------------------------------------------------------- records
     def records(self):
         """((key..., chunk id...), chunk ndarray) in key order (``tordd().sortByKey()``)."""
-        from bolt_amd.mi355x.dist import all_gather_bytes
+        from bolt_amd.mi355x.dist import gather_to_host
         ctx = self._ctx
         es = self._dtype.itemsize
         g = self._geom
-        if ctx.world_size > 1:
-            per = g.size * int(np.prod(self._shape[1:self._split], dtype=np.int64)) * es
-            sizes = [(hi - lo) * per for lo, hi in ctx.bounds(self._shape[0])]
-            buf = all_gather_bytes(ctx, self._packed, sizes)
-        else:
-            buf = self._packed
-        from bolt_amd.mi355x.dist import to_host
-        host = to_host(buf, self._dtype, (buf.numel() // self._dtype.itemsize,))
+        per = g.size * int(np.prod(self._shape[1:self._split], dtype=np.int64)) * es
+        sizes = [(hi - lo) * per for lo, hi in ctx.bounds(self._shape[0])]
+        host = gather_to_host(ctx, self._packed, sizes).view(self._dtype)
         kshape = self._shape[:self._split]
         ids = g.chunk_ids()
         for i, key in enumerate(np.ndindex(*kshape)):

@@ -130,12 +130,23 @@ def _offsets(sizes):
     return [int(v) for v in np.r_[0, np.cumsum([int(v) for v in sizes])][:-1]]
 
 
+def _drain_local(device):
+    """Wait (unbounded) for the local work queued on the current stream, so that
+    the bounded wait after an exchange times the exchange alone: a long
+    legitimate compute queue must not read as a failed peer."""
+    import torch
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(device))
+    ev.synchronize()
+
+
 def _rccl_all_gather(ctx, local, sizes):
     """bm_allgatherv on the current stream (include/bolt_mi355x.h), then a
     bounded wait for it (bm_comm_wait)."""
     import torch
     from bolt_amd.mi355x import _lib
     recv = _empty(sum(sizes), local.device)
+    _drain_local(local.device)
     stream = torch.cuda.current_stream(local.device).cuda_stream
     sp = local.data_ptr() if local.numel() else None
     rp = recv.data_ptr() if recv.numel() else None
@@ -161,6 +172,8 @@ def _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op):
     recv = _empty(sum(recv_sizes), send.device)
     cur = torch.cuda.current_stream(send.device)
     stream = ctx.comm_stream if async_op else cur
+    if not async_op:
+        _drain_local(send.device)
     if async_op:
         ready = torch.cuda.Event()
         ready.record(cur)
@@ -206,6 +219,45 @@ def all_to_all_bytes(ctx, send, send_sizes, recv_sizes, unit=1, async_op=False):
     if ctx.transport == "rccl":
         return _rccl_all_to_all(ctx, send, send_sizes, recv_sizes, async_op)
     return _test_all_to_all(ctx, send, send_sizes, recv_sizes, unit, async_op)
+
+
+# Egress across GPUs moves the global byte sequence in windows of at most this
+# many bytes: each window is one all_gather into a window-sized device buffer,
+# then a staged D2H into its place in the host result -- device memory per rank
+# stays at its slab plus one window, never the whole array (the reference
+# collects to the driver, bolt/spark/array.py:1006-1014).
+EGRESS_WINDOW = None  # None: 2 x the staging chunk (transfer.CHUNK); tests lower it
+
+
+def egress_window():
+    from bolt_amd.mi355x import transfer
+    return int(EGRESS_WINDOW) if EGRESS_WINDOW else 2 * transfer.CHUNK
+
+
+def gather_to_host(ctx, local, sizes, out=None):
+    """The concatenation of every rank's bytes (``sizes[r]`` bytes from rank r,
+    in rank order) as a host uint8 ndarray on every rank, gathered window by
+    window (EGRESS_WINDOW).  ``out``: a host uint8 array to fill instead."""
+    from bolt_amd.mi355x.transfer import copy_to_host
+    sizes = [int(v) for v in sizes]
+    total = sum(sizes)
+    if out is None:
+        out = np.empty(total, dtype=np.uint8)
+    if ctx.world_size == 1:
+        copy_to_host(local, out)
+        return out
+    offs = np.r_[0, np.cumsum(sizes)].astype(np.int64)
+    me = ctx.rank
+    w = max(1, egress_window())
+    for g0 in range(0, total, w):
+        g1 = min(total, g0 + w)
+        part = [max(0, min(g1, int(offs[r + 1])) - max(g0, int(offs[r]))) for r in range(ctx.world_size)]
+        lo = max(g0, int(offs[me])) - int(offs[me])
+        piece = local[lo:lo + part[me]] if part[me] else local[:0]
+        buf = all_gather_bytes(ctx, piece, part)
+        copy_to_host(buf, out[g0:g1])
+        del buf
+    return out
 
 
 # --- test executors only (transport "torch" / "host"; see the module docstring)

@@ -91,14 +91,35 @@ def to_host(t, dtype, shape):
     if t.device.type != "cuda":
         return t.numpy().view(dtype).reshape(shape)
     n = t.numel()
-    stream = torch.cuda.current_stream(t.device)
     if n <= SMALL:
         host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
         if n:
             host.copy_(t, non_blocking=True)
-            stream.synchronize()
+            torch.cuda.current_stream(t.device).synchronize()
         return host.numpy().view(dtype).reshape(shape)
     out = np.empty(n, dtype=np.uint8)
+    copy_to_host(t, out)
+    return out.view(dtype).reshape(shape)
+
+
+def copy_to_host(t, out):
+    """out[:] = the bytes of uint8 tensor ``t`` (``out`` a host uint8 ndarray of
+    t.numel() bytes), staged through two page-locked chunks: the host copy out
+    of chunk i overlaps the DMA of chunk i+1."""
+    import torch
+    n = t.numel()
+    if n == 0:
+        return
+    if t.device.type != "cuda":
+        out[:] = t.numpy()
+        return
+    stream = torch.cuda.current_stream(t.device)
+    if n <= SMALL:
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        host.copy_(t, non_blocking=True)
+        stream.synchronize()
+        _par_copy(out, host.numpy())
+        return
     bufs = [torch.empty(CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     evs = [torch.cuda.Event(), torch.cuda.Event()]
     starts = list(range(0, n, CHUNK))
@@ -116,7 +137,6 @@ def to_host(t, dtype, shape):
     lo = starts[-1]
     evs[(len(starts) - 1) % 2].synchronize()
     _par_copy(out[lo:n], bufs[(len(starts) - 1) % 2].numpy()[:n - lo])
-    return out.view(dtype).reshape(shape)
 
 
 def host_result(backend, nbytes, device):

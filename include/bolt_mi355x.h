@@ -125,19 +125,6 @@ int bm_permute(const void *src, void *dst, int ndim, const int64_t *shape,
                const int32_t *perm, int elem_bytes, void *stream);
 
 /*
- * Placement-adaptive tile order of the transposes behind bm_permute /
- * bm_copy_strided (no reference counterpart: Spark has no physical layout).
- * Two tile orders write the same bytes; which is faster depends on where the
- * source buffer's pages landed, so per (source buffer, copy shape) the library
- * times each once on the caller's stream and keeps the faster (no host wait;
- * BOLT_AMD_ADAPTIVE=0 disables it).
- * bm_tune_summary: out[0] = entries, out[1] = decided, out[2] = decided for
- * the staggered order.  bm_tune_reset: forget every decision.
- */
-int bm_tune_summary(int64_t *out);
-int bm_tune_reset(void);
-
-/*
  * bm_gather_rows -- dst[a, j, :] = src[a, idx[j], :] for a C-contiguous src
  * viewed as [n_outer][src_rows][row_bytes]; dst is [n_outer][n_idx][row_bytes].
  * idx is a DEVICE array of n_idx int64 row numbers in [0, src_rows) (the host

@@ -3,8 +3,10 @@ gloo on the CPU test executor: each rank builds its own shard with
 ConstructMI355X.fromshards, as bench.py does under torch.distributed.run, runs
 every op of every config, and checks the results against numpy on the global
 array.  A rehearsal of the driver's N-GPU scaling run (there over RCCL)."""
+import json
 import os
 import socket
+import subprocess
 import sys
 import traceback
 
@@ -96,10 +98,21 @@ def _body(rank, world):
             assert k2v.split == 2 and v2k.split == 4
             assert np.asarray(k2v.unchunk().toarray()).tobytes() == full.tobytes()
             assert np.asarray(v2k.unchunk().toarray()).tobytes() == full.tobytes()
-        # bench.py's post-timing check of the exchange, on shards made the bench's way
+        # bench.py's post-timing checks, on shards made the bench's way: the
+        # exchange (first op) and every permute bit for bit, every statistic
+        # over the sharded axis (C1's, C4's var, target64's mean / std) against
+        # the float64 truth of the global array
         t = bench.synth_shard(torch, shape, dt, torch.device("cpu"), 1234 + rank)
         tb = ConstructMI355X.fromshards(t.reshape(-1).view(torch.uint8), gshape, context=ctx, split=split, dtype=dt)
         assert bench.exchange_check(torch, cfg, tb, ctx, torch.device("cpu"), shape, dt, split), cfg
+        det, ok = bench.run_checks(torch, cfg, tb, ctx, torch.device("cpu"), shape, dt, world)
+        assert ok, (cfg, det)
+        names = [n for n, _, _ in bench.checks_of(cfg, tb)]
+        assert sorted(det) == sorted(names), (cfg, det)
+        stats = [n for n, _, spec in bench.checks_of(cfg, tb) if spec[0] == "stat"]
+        assert all(det[n].startswith("within rtol") for n in stats), det
+        if cfg in ("C4", "target64", "C1"):
+            assert stats, cfg  # the sharded-axis statistics are checked
 
 
 def _worker(rank, world, port, errq):
@@ -136,6 +149,92 @@ def test_bench_steps_weak_scaling(world):
     assert all(p.exitcode == 0 for p in procs)
 
 
+def test_stat_checks_catch_a_wrong_result(monkeypatch):
+    """The sharded-axis statistic check fails when the result is off by more
+    than the stated tolerance (here: one output nudged by 1e-9 relative, over
+    the float64 rtol of 1e-12)."""
+    sys.path[:0] = [HERE, ROOT]
+    import torch
+    import bench
+    truth = np.linspace(1.0, 2.0, 12)
+    ok, _ = bench.stat_within(truth.copy(), truth, truth.max(), "var")
+    assert ok
+    bad = truth.copy()
+    bad[5] *= 1 + 1e-9
+    ok, worst = bench.stat_within(bad, truth, truth.max(), "var")
+    assert not ok and worst > 1
+    ok, _ = bench.stat_within(truth.astype(np.float32), truth, 2.0, "mean")
+    assert ok  # float32 output: rtol 1e-6
+    del torch
+
+
+SHAPES = json.dumps({"C2": [4, 8, 8], "C3": [2, 3, 4, 8], "C4": [6, 16, 16], "C5": [2, 2, 2, 20, 20],
+                     "target64": [2, 3, 4, 8]})
+
+
+def _bench(args, env_extra, timeout=600):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_its_ranks(world):
+    """`bench.py --gpus N` without WORLD_SIZE starts the N rank processes itself
+    and rank 0's JSON line comes back: n_gpus N, every check bit-exact /
+    within tolerance, the C4 sub-record's sharded-axis var included (the CPU
+    rehearsal: test executor over gloo, tiny per-rank shapes)."""
+    r = _bench(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--no-pmc", "--no-cpu-baseline",
+                "--shard-shapes", SHAPES],
+               {"BOLT_AMD_BENCH_BACKEND": "gloo", "BOLT_AMD_BENCH_DEVICE": "cpu"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["launcher"].startswith("bench.py --gpus %d" % world)
+    assert d["exchange_check"] == "bit-exact"
+    assert d["config"]["global_shape"][0] == 4 * world
+    for cfg in ("C3", "C4", "C5"):
+        c = d["configs"][cfg]
+        assert c["checks"]["all"].startswith("every result matches"), (cfg, c["checks"])
+        assert c["global_shape"][0] == json.loads(SHAPES)[cfg][0] * world
+    assert d["configs"]["C4"]["checks"]["var"].startswith("within rtol 1e-12")
+    assert "target64" not in d  # the 64 GiB target is a one-GPU record
+
+
+def test_bench_refuses_gpu_count_mismatch():
+    """More GPUs than visible (none here) without the rehearsal knobs, or a
+    --gpus that differs from WORLD_SIZE: exit 2, nothing measured."""
+    r = _bench(["--gpus", "2", "--steps", "1"], {}, timeout=120)
+    assert r.returncode == 2 and "refusing" in r.stderr and not r.stdout.strip()
+    r = _bench(["--gpus", "3", "--steps", "1"], {"WORLD_SIZE": "2"}, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and not r.stdout.strip()
+
+
+def test_bench_one_rank_rehearsal_record():
+    """The default run's record on one rank (CPU rehearsal): the headline line,
+    stats_roofline for mean / std, target64 and the C3 / C4 / C5 sub-records
+    with per-op time and fraction of peak, and the checks."""
+    r = _bench(["--steps", "2", "--warmup", "1", "--no-pmc", "--no-cpu-baseline", "--target-steps", "1",
+                "--shard-shapes", SHAPES], {"BOLT_AMD_BENCH_DEVICE": "cpu"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and set(d["stats_roofline"]) >= {"mean", "std"}
+    assert d["stats_roofline"]["mean"]["launches_per_call"] == 1.0
+    assert d["checks"]["swap"] == "bit-exact"
+    t = d["target64"]
+    assert t["checks"]["mean"].startswith("within rtol 1e-6") and t["checks"]["swap"] == "bit-exact"
+    for cfg, ops in (("C3", {"swap", "T"}), ("C4", {"swap", "chunk", "unchunk", "var"}),
+                     ("C5", {"T", "transpose", "chunk", "unchunk", "keys_to_values", "values_to_keys"})):
+        c = d["configs"][cfg]
+        assert set(c["ops"]) == ops and c["dominant"] in ops
+        assert all(o["ms"] is None or o["ms"] > 0 for o in c["ops"].values())
+        assert c["checks"]["all"].startswith("every result matches")
+
+
 @pytest.mark.parametrize("cfg,shape,dtype", [
     ("C3", (4, 8, 8, 32), np.float32), ("C4", (6, 16, 16), np.uint16),
     ("C5", (2, 4, 4, 4, 4), np.float64), ("target64", (4, 8, 8, 32), np.float32)])
@@ -147,4 +246,20 @@ def test_local_numpy_baseline_fields(cfg, shape, dtype, monkeypatch):
     monkeypatch.setitem(bench.LOCAL_SAMPLE_ROWS, cfg, 2)
     r = bench.cpu_baseline(cfg, shape, dtype, rows=None)
     assert r["unit"] == "GB/s" and r["cores"] == 1 and r["kind"] == "port"
-    assert r["value"] > 0 and "(2," in r["sample"]
+    assert r["value"] > 0 and "(2," in r["sample"] and r["reps"] == 3 and "best of 3" in r["sample"]
+
+
+def test_c2_cpu_baseline_method(monkeypatch):
+    """SURVEY 8(d)'s method on every C2 CPU line: best of 3 after 1 warm-up;
+    the OpenMP line states its threads and why they are fewer than the host's."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    r = bench.cpu_baseline("C2", (6, 8, 8), np.float32, rows=4)
+    assert r["reps"] == 3 and r["local_numpy"]["reps"] == 3 and r["spark_local8"]["reps"] == 3
+    assert "best of 3 after 1 warm-up" in r["sample"]
+    omp = r["openmp"]
+    if omp.get("value") is not None:
+        assert omp["reps"] == 3 and omp["cores"] == 2 and omp["affinity_cpus"] >= 1
+        if (os.cpu_count() or 1) > 2:
+            assert "OMP_NUM_THREADS=2" in omp["cores_reason"]
