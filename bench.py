@@ -482,7 +482,7 @@ def exchange_check(torch, cfg, b, ctx, dev, shape=None, dtype=None, split=None):
 
 def _library_kernel(name):
     import re
-    return re.search(r"(?<![A-Za-z0-9_])k_(transpose|rowcopy|generic|red|recmap|gather)", name) is not None
+    return re.search(r"(?<![A-Za-z0-9_])k_(transpose|rowcopy|generic|red|recmap|record|gather)", name) is not None
 
 
 def pmc_traffic(cfg, args, nops, warmup=1, steps=2):
@@ -826,7 +826,7 @@ def make_event(dev):
     return torch.cuda.Event(enable_timing=True) if dev.type == "cuda" else HostEvent()
 
 
-LAUNCHES = ("permute", "copy_strided", "gather_rows", "record_gather", "record_scatter", "reduce",
+LAUNCHES = ("permute", "copy_strided", "gather_rows", "record_gather", "record_scatter", "record_runs", "reduce",
             "reduce_state", "reduce_combine")
 
 

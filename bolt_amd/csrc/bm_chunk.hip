@@ -330,6 +330,73 @@ void launch_scatter(const char *src, char *dst, const int32_t *ma, const int32_t
     k_recmap_scatter<ES, 1><<<(int)g, kCThreads, 0, st>>>(src, dst, ma, mb, total, fv, fg, gstride);
 }
 
+// Record runs: the same moves as the record scatter when a source record is a
+// handful of long runs (C5 keys_to_values((2,)): 16 chunk boxes of 2.6-3.2 KB,
+// each contiguous in the source record and in its new record).  Run b of
+// record r (r = g * group + k):
+//     dst[g * gstride + a_b + k * m_b + j] = src[r * src_rec + s_b + j],  j < len_b
+// One wave per (record, run) unit, no maps: every lane's loads issue at once,
+// U vectors in flight per lane, and a wave writes one contiguous run.
+// DMAJOR: units ordered by destination (the group's runs b, then k), so the
+// waves in flight write consecutive runs of one new record; else by source.
+// Runs table: DEVICE int64 [s, len, a, m] x nruns, in VB-byte vectors.
+#ifndef BM_RUNS_U
+#define BM_RUNS_U 4
+#endif
+#ifndef BM_RUNS_DMAJOR
+#define BM_RUNS_DMAJOR 0
+#endif
+template <int VB, int U, bool DMAJOR>
+__global__ void __launch_bounds__(kCThreads)
+    k_record_runs(const char *__restrict__ src, char *__restrict__ dst, const int64_t *__restrict__ runs,
+                  int nruns, uint64_t nunits, int64_t src_rec, int64_t gstride, FastDiv fruns, FastDiv fgroup) {
+  typedef typename VecB<VB>::t V;
+  const V *s = reinterpret_cast<const V *>(src);
+  V *d = reinterpret_cast<V *>(dst);
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (kCThreads / 64);
+  for (uint64_t u = (uint64_t)blockIdx.x * (kCThreads / 64) + (threadIdx.x >> 6); u < nunits; u += nw) {
+    uint64_t r, g, k;
+    int b;
+    if (DMAJOR) {  // u = (g * nruns + b) * group + k
+      const uint64_t q = fd_div(u, fgroup);
+      k = u - q * fgroup.d;
+      g = fd_div(q, fruns);
+      b = (int)(q - g * fruns.d);
+      r = g * fgroup.d + k;
+    } else {  // u = r * nruns + b
+      r = fd_div(u, fruns);
+      b = (int)(u - r * fruns.d);
+      g = fd_div(r, fgroup);
+      k = r - g * fgroup.d;
+    }
+    const int64_t *e = runs + 4 * b;
+    const int64_t len = e[1];
+    const V *sp = s + (int64_t)r * src_rec + e[0];
+    V *dp = d + (int64_t)g * gstride + e[2] + (int64_t)k * e[3];
+    for (int64_t v0 = lane; v0 < len; v0 += 64 * U) {
+      V x[U];
+#pragma unroll
+      for (int t = 0; t < U; ++t)
+        if (v0 + 64 * t < len) x[t] = ld_src(sp + v0 + 64 * t);
+#pragma unroll
+      for (int t = 0; t < U; ++t)
+        if (v0 + 64 * t < len) st_dst(x[t], dp + v0 + 64 * t);
+    }
+  }
+}
+
+template <int VB>
+void launch_runs(const char *src, char *dst, const int64_t *runs, int nruns, int64_t nrec, int64_t src_rec,
+                 int64_t group, int64_t gstride, hipStream_t st) {
+  const uint64_t nunits = (uint64_t)nrec * (uint64_t)nruns;
+  uint64_t g = (nunits + kCThreads / 64 - 1) / (kCThreads / 64);
+  if (g > 1048576) g = 1048576;  // then grid-stride over units
+  const FastDiv fr = make_fastdiv((uint64_t)nruns), fg = make_fastdiv((uint64_t)group);
+  k_record_runs<VB, BM_RUNS_U, BM_RUNS_DMAJOR != 0><<<(int)g, kCThreads, 0, st>>>(
+      src, dst, runs, nruns, nunits, src_rec, gstride, fr, fg);
+}
+
 struct Launch {
   const char *src;
   char *dst;
@@ -540,6 +607,47 @@ extern "C" int bm_record_scatter(const void *src_, void *dst_, int64_t nrec, int
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     bm_set_error("bm_record_scatter: launch failed: %s", hipGetErrorString(e));
+    return BM_E_HIP;
+  }
+  return BM_OK;
+}
+
+extern "C" int bm_record_runs(const void *src_, void *dst_, int64_t nrec, int64_t src_rec, int64_t group,
+                              int64_t dst_group_stride, int nruns, const int64_t *runs, int vec_bytes,
+                              int elem_bytes, void *stream) {
+  const int es = elem_bytes, vb = vec_bytes;
+  if (nrec < 0 || src_rec <= 0 || group < 1 || nrec % group || dst_group_stride < 0 || nruns < 1 ||
+      nruns > 4096 || (es != 1 && es != 2 && es != 4 && es != 8) || vb < es || vb > 16 || (vb & (vb - 1)) ||
+      (src_rec * es) % vb || (dst_group_stride * es) % vb) {
+    bm_set_error("bm_record_runs: bad arguments (nrec %lld, src_rec %lld, group %lld, stride %lld, nruns %d, "
+                 "vec_bytes %d, elem_bytes %d)", (long long)nrec, (long long)src_rec, (long long)group,
+                 (long long)dst_group_stride, nruns, vb, es);
+    return BM_E_ARG;
+  }
+  if (nrec == 0) return BM_OK;
+  if (!src_ || !dst_ || !runs) {
+    bm_set_error("bm_record_runs: null pointer");
+    return BM_E_ARG;
+  }
+  if ((uintptr_t)src_ % (uintptr_t)vb || (uintptr_t)dst_ % (uintptr_t)vb) {
+    bm_set_error("bm_record_runs: buffers not aligned to %d-byte vectors", vb);
+    return BM_E_ARG;
+  }
+  const char *src = static_cast<const char *>(src_);
+  char *dst = static_cast<char *>(dst_);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // record size and group stride in vectors; the table is in vectors already
+  const int64_t sv = src_rec * es / vb, gv = dst_group_stride * es / vb;
+  switch (vb) {
+    case 16: launch_runs<16>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
+    case 8: launch_runs<8>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
+    case 4: launch_runs<4>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
+    case 2: launch_runs<2>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
+    default: launch_runs<1>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    bm_set_error("bm_record_runs: launch failed: %s", hipGetErrorString(e));
     return BM_E_HIP;
   }
   return BM_OK;

@@ -40,6 +40,8 @@ SIGNATURES = {
                                            _c.c_void_p]),
     "bm_record_scatter": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,
                                      _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_void_p]),
+    "bm_record_runs": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64,
+                                  _c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_void_p]),
     "bm_reduce_workspace_bytes": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int64, _c.c_int64,
                                              _c.c_int64, _c.POINTER(_c.c_size_t)]),
     "bm_reduce": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64,

@@ -240,6 +240,32 @@ class HipBackend(object):
                                               ctypes.c_void_p(db.data_ptr()) if db is not None else None,
                                               vec, int(es), self._stream(src)), "bm_record_scatter")
 
+    def record_runs(self, src, src_off, dst, dst_off, nrec, src_rec, group, gstride, runs, key, es):
+        """Run b of record r = g*group + k: dst[g*gstride + a_b + k*m_b + j] =
+        src[r*src_rec + s_b + j], j < len_b (bm_record_runs; runs = (table
+        [s, len, a, m] in vec_bytes vectors, vec_bytes) from
+        plan.scatter_to_runs, checked here against the record and destination
+        sizes and uploaded once per (device, key))."""
+        import torch
+        ck = (src.device, key)
+        hit = self._maps.get(ck)
+        if hit is None:
+            table, vb = runs
+            t = np.ascontiguousarray(table, dtype=np.int64).reshape(-1, 4)
+            per = vb // int(es)
+            s0, ln, a, m = t[:, 0] * per, t[:, 1] * per, t[:, 2] * per, t[:, 3] * per
+            if (t.size == 0 or (ln <= 0).any() or (s0 < 0).any() or (s0 + ln > src_rec).any() or (a < 0).any()
+                    or (m < 0).any() or (a + (group - 1) * m + ln > gstride).any()):
+                raise ValueError("record runs do not fit the records")
+            hit = (torch.from_numpy(t.reshape(-1).copy()).to(src.device), t.shape[0], int(vb))
+            if len(self._maps) >= 256:
+                self._drop_maps(src.device)
+            self._maps[ck] = hit
+        table, n, vb = hit
+        _lib.check(self.lib.bm_record_runs(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec), int(src_rec),
+                                           int(group), int(gstride), int(n), ctypes.c_void_p(table.data_ptr()),
+                                           vb, int(es), self._stream(src)), "bm_record_runs")
+
     def _workspace(self, stat, code, O, R, I, device):
         import torch
         key = (stat, code, O, R, I)

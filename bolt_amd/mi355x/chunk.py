@@ -65,6 +65,25 @@ def _scatter_plan(key, build, src_rec, gstride, es):
     return plan
 
 
+def _use_runs():
+    """keys_to_values whose records are a few long runs as bm_record_runs (A/B
+    knob BOLT_AMD_RUNS=0: the map scatter)."""
+    return os.environ.get("BOLT_AMD_RUNS", "1") != "0"
+
+
+_RUNS_PLANS = {}
+
+
+def _runs_plan(key, plan, src_rec, gstride, es):
+    """(runs, vec_bytes) of a scatter plan (plan.scatter_to_runs), cached per key."""
+    from bolt_amd.mi355x.plan import scatter_to_runs
+    if key not in _RUNS_PLANS:
+        if len(_RUNS_PLANS) > 256:
+            _RUNS_PLANS.clear()
+        _RUNS_PLANS[key] = scatter_to_runs(plan[0], plan[1], src_rec, gstride, es)
+    return _RUNS_PLANS[key]
+
+
 def _use_record_map(src_rec, es):
     """Small records: one record-map gather instead of a strided copy per chunk run."""
     if os.environ.get("BOLT_AMD_RECORD_MAP", "1") == "0":  # A/B knob
@@ -305,8 +324,15 @@ class ChunkedArrayMI355X(object):
                 if plan is not None:
                     nold = int(np.prod(lk, dtype=np.int64))
                     packed = _empty(nold // K * new.size * es, self._packed.device)
-                    self._backend.record_scatter(self._packed, 0, packed, 0, nold, g.size, K, new.size, plan,
-                                                 ("scatter", "k2v", es, K) + g.key() + new.key(), es)
+                    key = ("k2v", es, K) + g.key() + new.key()
+                    runs = _runs_plan(key, plan, g.size, new.size, es) if _use_runs() else None
+                    if runs is not None:
+                        # every old record is a few chunk boxes: one wave per box
+                        self._backend.record_runs(self._packed, 0, packed, 0, nold, g.size, K, new.size, runs,
+                                                  ("runs",) + key, es)
+                    else:
+                        self._backend.record_scatter(self._packed, 0, packed, 0, nold, g.size, K, new.size, plan,
+                                                     ("scatter",) + key, es)
                     return self._constructor(packed, shape=newshape, split=newsplit, dtype=self._dtype,
                                              plan=newplan, padding=newpadding, ordered=True, context=self._ctx)
             copies = k2v_copies(self._geom, new, lk, kmask)

@@ -404,6 +404,37 @@ def scatter_vec(map_a, map_b, src_rec, gstride, es):
     return 1
 
 
+def scatter_to_runs(map_a, map_b, src_rec, gstride, es, max_runs=64, min_bytes=1024):
+    """A scatter plan whose kept elements form a few long runs -> the runs
+    table of bm_record_runs, or None: (runs, vec_bytes) with runs an int64
+    array [s, len, a, m] x nruns in vec_bytes-byte vectors.  A run is a
+    maximal stretch of source elements landing consecutively with one group
+    step m.  Taken when there are at most ``max_runs`` runs of ``min_bytes``
+    or more on average (C5 keys_to_values((2,)): 16 chunk boxes of 2.6-3.2 KB);
+    short runs (unchunk's 128-B rows) keep the map scatter."""
+    a = np.asarray(map_a, dtype=np.int64)
+    b = np.asarray(map_b, dtype=np.int64)
+    keep = a >= 0
+    if not keep.any():
+        return None
+    cont = np.zeros(a.size, dtype=bool)
+    cont[1:] = keep[1:] & keep[:-1] & (a[1:] == a[:-1] + 1) & (b[1:] == b[:-1])
+    first = keep & ~cont
+    starts = np.flatnonzero(first)
+    if starts.size > max_runs:
+        return None
+    lens = np.bincount((np.cumsum(first) - 1)[keep], minlength=starts.size).astype(np.int64)
+    if np.mean(lens) * es < min_bytes:
+        return None
+    runs = np.stack([starts, lens, a[starts], b[starts]], axis=1).astype(np.int64)
+    vb = 16
+    while vb > es and (np.any((runs * es) % vb) or (src_rec * es) % vb or (gstride * es) % vb):
+        vb //= 2
+    if vb < es or np.any((runs * es) % vb):
+        return None
+    return runs * es // vb, int(vb)
+
+
 def scatter_runs_ok(map_a, map_b, es):
     """Whether a record scatter writes whole lines: its destination runs
     (consecutive kept elements landing consecutively) are all 128-B aligned

@@ -215,6 +215,22 @@ int bm_record_scatter(const void *src, void *dst, int64_t nrec, int64_t src_rec,
                       int64_t group, int64_t dst_group_stride, const int32_t *map_a,
                       const int32_t *map_b, int vec, int elem_bytes, void *stream);
 
+/*
+ * bm_record_runs -- bm_record_scatter's moves when every source record is a
+ * few long runs (no maps): run b of record r = g * group + k is copied whole,
+ *     dst[g * dst_group_stride + a_b + k * m_b + j] = src[r * src_rec + s_b + j]
+ * for j < len_b.  runs: DEVICE int64 array [s_b, len_b, a_b, m_b] x nruns,
+ * in units of vec_bytes-byte vectors (vec_bytes a power of two in
+ * [elem_bytes, 16] dividing every record, stride and run; the caller checks
+ * the runs lie inside the records and the destination).  src_rec and
+ * dst_group_stride are in elements; nrec must be a multiple of group.
+ * C5's keys_to_values((2,)): 16 chunk boxes of 2.6-3.2 KB per record, one
+ * wave per box (bolt/spark/chunk.py:202-289).  Bit-exact.
+ */
+int bm_record_runs(const void *src, void *dst, int64_t nrec, int64_t src_rec,
+                   int64_t group, int64_t dst_group_stride, int nruns,
+                   const int64_t *runs, int vec_bytes, int elem_bytes, void *stream);
+
 int bm_reduce_workspace_bytes(int stat, int in_dtype, int64_t O, int64_t R,
                               int64_t I, size_t *bytes);
 

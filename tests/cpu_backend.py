@@ -92,6 +92,19 @@ class CpuBackend(object):
         assert idx.min(initial=0) >= 0 and idx.max(initial=-1) < d.size
         d[idx.reshape(-1)] = s[:, keep].reshape(-1)
 
+    def record_runs(self, src, src_off, dst, dst_off, nrec, src_rec, group, gstride, runs, key, es):
+        if nrec == 0:
+            return
+        table, vb = runs
+        t = np.asarray(table, dtype=np.int64).reshape(-1, 4) * (vb // es)
+        dt = np.dtype((np.void, es))
+        s = _np(src)[src_off:src_off + nrec * src_rec * es].view(dt).reshape(nrec, src_rec)
+        d = _np(dst)[dst_off:dst_off + nrec // group * gstride * es].view(dt).reshape(nrec // group, gstride)
+        for s0, ln, a, m in t:
+            assert s0 >= 0 and s0 + ln <= src_rec and a + (group - 1) * m + ln <= gstride
+            for k in range(group):
+                d[:, a + k * m:a + k * m + ln] = s[k::group, s0:s0 + ln]
+
     def permute(self, src, shape, perm, es, dst):
         a = _np(src).view(np.dtype((np.void, es))).reshape(tuple(shape))
         out = _np(dst).view(np.dtype((np.void, es)))

@@ -233,3 +233,58 @@ def test_scatter_plans_invert_the_gather_maps():
     assert scatter_runs_ok(m[0], m[1], 8)
     runs18 = np.concatenate([np.arange(18) + 20 * k for k in range(4)]).astype(np.int32)
     assert not scatter_runs_ok(runs18, np.zeros(72, np.int32), 8)
+
+
+RUNS_CASES = [
+    # (shape, split, dtype, plan, padding): keys_to_values of the trailing key
+    # whose chunk boxes are long runs (bm_record_runs), every vector width
+    ((2, 3, 4, 40, 40), 3, np.float64, (20, 20), (2, 2)),   # C5-like: 16-B vectors, 3.9-KB boxes
+    ((2, 3, 2, 36, 30), 3, np.float32, (18, 15), (1, 1)),   # 1.2-1.4-KB boxes
+    ((2, 2, 3, 64, 64), 3, np.uint8, (48, 48), (1, 1)),     # odd box sizes: 1-B vectors
+    ((3, 5, 64, 48), 2, np.int16, (64, 24), (0, 2)),        # 2 key axes, 1 moved
+]
+
+
+@pytest.mark.parametrize("shape,split,dtype,plan,pad", RUNS_CASES)
+def test_record_runs_path_matches(bctx, monkeypatch, shape, split, dtype, plan, pad):
+    """keys_to_values through bm_record_runs gives the same packed bytes as the
+    map scatter and the strided copies, and unchunks to the input."""
+    from bolt_amd.mi355x import _ops
+    rng = np.random.default_rng(8)
+    x = rng.integers(0, 250, size=shape).astype(dtype)
+    calls = []
+    be = _ops.backend_for(bctx.device)
+    orig = be.record_runs
+    monkeypatch.setattr(be, "record_runs", lambda *a, **k: (calls.append(a[4:8]), orig(*a, **k))[1])
+    out = {}
+    for runs, scatter in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("BOLT_AMD_RUNS", runs)
+        monkeypatch.setenv("BOLT_AMD_SCATTER", scatter)
+        c = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad)
+        k = c.keys_to_values((split - 1,))
+        out[runs + scatter] = (k._packed.cpu().numpy().tobytes(), k.unchunk().toarray().tobytes())
+    assert calls, "the runs path was not taken"
+    assert out["11"] == out["01"] == out["00"]
+    want = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad).keys_to_values(
+        (split - 1,)).unchunk().toarray()
+    assert out["11"][1] == np.asarray(want).tobytes()
+
+
+def test_scatter_to_runs_table():
+    """plan.scatter_to_runs: C5's k2v plan is 16 runs (one per chunk box) in
+    16-B vectors; unchunk's 128-B rows stay with the map scatter; odd sizes
+    narrow the vector."""
+    from bolt_amd.mi355x.plan import (ChunkGeometry, copies_to_scatter, k2v_copies, scatter_to_runs)
+    g = ChunkGeometry((64, 64), (16, 16), (2, 2))
+    new = ChunkGeometry((64, 64, 64), (64, 16, 16), (0, 2, 2))
+    sc = copies_to_scatter(k2v_copies(g, new, [1, 1, 64], np.array([False, False, True])), 64 * g.size,
+                           group=64, src_rec=g.size)
+    runs, vb = scatter_to_runs(sc[0], sc[1], g.size, new.size, 8)
+    assert vb == 16 and runs.shape == (16, 4)
+    lens = sorted(set((runs[:, 1] * 16).tolist()))
+    assert lens == [2592, 2880, 3200]            # 18x18, 18x20 / 20x18, 20x20 float64 boxes
+    assert np.array_equal(runs[:, 1], runs[:, 3])  # consecutive keys stack whole boxes
+    un = copies_to_scatter([(sh, ps, ds, po, do) for sh, ds, ps, do, po in g.copies(unpack=True)], g.size)
+    assert scatter_to_runs(un[0], un[1], g.size, 64 * 64, 8) is None
+    a = np.arange(1089, dtype=np.int32)
+    assert scatter_to_runs(a, np.zeros_like(a), 1089, 1089, 1)[1] == 1

@@ -35,6 +35,10 @@ def load(path):
         lib.bm_record_scatter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    if hasattr(lib, "bm_record_runs"):
+        lib.bm_record_runs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p]
     if hasattr(lib, "bm_record_gather_masked"):
         lib.bm_record_gather_masked.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                                 ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, I64P,
@@ -203,6 +207,43 @@ class RecScatter(object):
         assert rc == 0, lib.bm_last_error()
 
 
+class RecRuns(object):
+    """C5's keys_to_values((2,)) as bm_record_runs: one wave per chunk box
+    (plan.scatter_to_runs of the scatter plan)."""
+
+    def __init__(self):
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bolt_amd.mi355x import plan
+        g = plan.ChunkGeometry((64, 64), (16, 16), (2, 2))
+        new = plan.ChunkGeometry((64, 64, 64), (64, 16, 16), (0, 2, 2))
+        self.nrec, self.src_rec, self.group, self.gstride = 64 ** 3, g.size, 64, new.size
+        map_a, map_b = plan.copies_to_scatter(plan.k2v_copies(g, new, [1, 1, 64], np.array([False, False, True])),
+                                              64 * g.size, group=64, src_rec=g.size)
+        runs, self.vb = plan.scatter_to_runs(map_a, map_b, g.size, new.size, 8)
+        self.runs_host = runs * (self.vb // 8)
+        self.n = runs.shape[0]
+        self.table = torch.from_numpy(runs.reshape(-1).copy()).cuda()
+        self.src = torch.randint(0, 255, (self.nrec * g.size * 8,), dtype=torch.uint8, device="cuda")
+        self.dst = torch.empty(self.nrec // 64 * new.size * 8, dtype=torch.uint8, device="cuda")
+        self.bytes = self.src.numel() + self.dst.numel()
+
+    def __call__(self, lib):
+        rc = lib.bm_record_runs(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
+                                self.nrec, self.src_rec, self.group, self.gstride, self.n,
+                                ctypes.c_void_p(self.table.data_ptr()), self.vb, 8, stream())
+        assert rc == 0, lib.bm_last_error()
+
+    def check(self):
+        s = self.src.view(torch.int64).view(self.nrec, self.src_rec)
+        d = self.dst.view(torch.int64).view(self.nrec // self.group, self.gstride)
+        for s0, ln, a, m in self.runs_host:
+            for k in range(self.group):
+                if not torch.equal(d[:, a + k * m:a + k * m + ln], s[k::self.group, s0:s0 + ln]):
+                    return False
+        return True
+
+
 class Unchunk(object):
     """C5's unchunk as the strided copies of the chunk geometry (one per run combination)."""
 
@@ -251,6 +292,7 @@ class K2V(object):
 OPS = {
     "c5_k2v": lambda: K2V(),
     "c5_k2v_scatter": lambda: RecScatter("k2v"),
+    "c5_k2v_runs": lambda: RecRuns(),
     "c5_v2k_scatter": lambda: RecScatter("v2k"),
     "c5_unchunk": lambda: Unchunk(),
     "c5_unchunk_scatter": lambda: RecScatter("unchunk"),
