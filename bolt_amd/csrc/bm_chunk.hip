@@ -386,9 +386,74 @@ __global__ void __launch_bounds__(kCThreads)
   }
 }
 
+// Destination walk (runs tile each new record: m_b = len_b, regions
+// [a_b, a_b + group * len_b) back to back): lanes take the destination vectors
+// in order -- every wave writes 64 * U consecutive vectors, whole lines -- and
+// each finds its source: run b by binary search over the runs (sorted by a,
+// staged in LDS), k = (o - a_b) / len_b, then the source record g * group + k.
+#ifndef BM_RUNS_DWALK
+#define BM_RUNS_DWALK 1
+#endif
+#ifndef BM_RUNS_DWALK_U
+#define BM_RUNS_DWALK_U 2
+#endif
+constexpr int kMaxWalkRuns = 64;
+template <int VB, int U>
+__global__ void __launch_bounds__(kCThreads)
+    k_record_runs_dst(const char *__restrict__ src, char *__restrict__ dst, const int64_t *__restrict__ runs,
+                      int nruns, uint64_t total, int64_t src_rec, int64_t group, FastDiv fgs) {
+  typedef typename VecB<VB>::t V;
+  __shared__ int64_t tab[4 * kMaxWalkRuns];
+  __shared__ double inv[kMaxWalkRuns];
+  for (int i = threadIdx.x; i < 4 * nruns; i += kCThreads) tab[i] = runs[i];
+  for (int i = threadIdx.x; i < nruns; i += kCThreads) inv[i] = 1.0 / (double)runs[4 * i + 1];
+  __syncthreads();
+  const V *s = reinterpret_cast<const V *>(src);
+  V *d = reinterpret_cast<V *>(dst);
+  const int lane = threadIdx.x & 63;
+  const uint64_t per_block = (uint64_t)kCThreads * U;
+  const uint64_t wave0 = (uint64_t)(threadIdx.x >> 6) * 64 * U;
+  for (uint64_t base = (uint64_t)blockIdx.x * per_block; base < total; base += (uint64_t)gridDim.x * per_block) {
+    V x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t j = base + wave0 + (uint64_t)u * 64 + lane;
+      if (j < total) {
+        const uint64_t g = fd_div(j, fgs);
+        const int64_t o = (int64_t)(j - g * fgs.d);
+        int lo = 0, hi = nruns - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (tab[4 * mid + 2] <= o) lo = mid;
+          else hi = mid - 1;
+        }
+        const int64_t off = o - tab[4 * lo + 2], len = tab[4 * lo + 1];
+        int64_t k = (int64_t)((double)off * inv[lo]);
+        if (k * len > off) --k;
+        else if ((k + 1) * len <= off) ++k;
+        x[u] = ld_src(s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + (off - k * len));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t j = base + wave0 + (uint64_t)u * 64 + lane;
+      if (j < total) st_dst(x[u], d + j);
+    }
+  }
+}
+
 template <int VB>
 void launch_runs(const char *src, char *dst, const int64_t *runs, int nruns, int64_t nrec, int64_t src_rec,
-                 int64_t group, int64_t gstride, hipStream_t st) {
+                 int64_t group, int64_t gstride, bool tiled, hipStream_t st) {
+  if (BM_RUNS_DWALK && tiled) {
+    const uint64_t total = (uint64_t)(nrec / group) * (uint64_t)gstride;
+    const uint64_t per_block = (uint64_t)kCThreads * BM_RUNS_DWALK_U;
+    uint64_t g = (total + per_block - 1) / per_block;
+    if (g > 1048576) g = 1048576;
+    k_record_runs_dst<VB, BM_RUNS_DWALK_U><<<(int)g, kCThreads, 0, st>>>(src, dst, runs, nruns, total, src_rec,
+                                                                        group, make_fastdiv((uint64_t)gstride));
+    return;
+  }
   const uint64_t nunits = (uint64_t)nrec * (uint64_t)nruns;
   uint64_t g = (nunits + kCThreads / 64 - 1) / (kCThreads / 64);
   if (g > 1048576) g = 1048576;  // then grid-stride over units
@@ -613,15 +678,17 @@ extern "C" int bm_record_scatter(const void *src_, void *dst_, int64_t nrec, int
 }
 
 extern "C" int bm_record_runs(const void *src_, void *dst_, int64_t nrec, int64_t src_rec, int64_t group,
-                              int64_t dst_group_stride, int nruns, const int64_t *runs, int vec_bytes,
+                              int64_t dst_group_stride, int nruns, const int64_t *runs, int vec_bytes, int flags,
                               int elem_bytes, void *stream) {
   const int es = elem_bytes, vb = vec_bytes;
+  const bool tiled = (flags & BM_RUNS_TILED) != 0;
   if (nrec < 0 || src_rec <= 0 || group < 1 || nrec % group || dst_group_stride < 0 || nruns < 1 ||
-      nruns > 4096 || (es != 1 && es != 2 && es != 4 && es != 8) || vb < es || vb > 16 || (vb & (vb - 1)) ||
+      nruns > 4096 || (tiled && nruns > kMaxWalkRuns) || (flags & ~BM_RUNS_TILED) ||
+      (es != 1 && es != 2 && es != 4 && es != 8) || vb < es || vb > 16 || (vb & (vb - 1)) ||
       (src_rec * es) % vb || (dst_group_stride * es) % vb) {
     bm_set_error("bm_record_runs: bad arguments (nrec %lld, src_rec %lld, group %lld, stride %lld, nruns %d, "
-                 "vec_bytes %d, elem_bytes %d)", (long long)nrec, (long long)src_rec, (long long)group,
-                 (long long)dst_group_stride, nruns, vb, es);
+                 "vec_bytes %d, flags %d, elem_bytes %d)", (long long)nrec, (long long)src_rec, (long long)group,
+                 (long long)dst_group_stride, nruns, vb, flags, es);
     return BM_E_ARG;
   }
   if (nrec == 0) return BM_OK;
@@ -639,11 +706,11 @@ extern "C" int bm_record_runs(const void *src_, void *dst_, int64_t nrec, int64_
   // record size and group stride in vectors; the table is in vectors already
   const int64_t sv = src_rec * es / vb, gv = dst_group_stride * es / vb;
   switch (vb) {
-    case 16: launch_runs<16>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
-    case 8: launch_runs<8>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
-    case 4: launch_runs<4>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
-    case 2: launch_runs<2>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
-    default: launch_runs<1>(src, dst, runs, nruns, nrec, sv, group, gv, st); break;
+    case 16: launch_runs<16>(src, dst, runs, nruns, nrec, sv, group, gv, tiled, st); break;
+    case 8: launch_runs<8>(src, dst, runs, nruns, nrec, sv, group, gv, tiled, st); break;
+    case 4: launch_runs<4>(src, dst, runs, nruns, nrec, sv, group, gv, tiled, st); break;
+    case 2: launch_runs<2>(src, dst, runs, nruns, nrec, sv, group, gv, tiled, st); break;
+    default: launch_runs<1>(src, dst, runs, nruns, nrec, sv, group, gv, tiled, st); break;
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

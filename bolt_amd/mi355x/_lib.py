@@ -41,7 +41,7 @@ SIGNATURES = {
     "bm_record_scatter": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64,
                                      _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_int, _c.c_void_p]),
     "bm_record_runs": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64,
-                                  _c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_void_p]),
+                                  _c.c_int, _c.c_void_p, _c.c_int, _c.c_int, _c.c_int, _c.c_void_p]),
     "bm_reduce_workspace_bytes": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int64, _c.c_int64,
                                              _c.c_int64, _c.POINTER(_c.c_size_t)]),
     "bm_reduce": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64,
@@ -65,6 +65,7 @@ SIGNATURES = {
     "bm_comm_abort": (_c.c_int, [_c.c_void_p]),
 }
 COMM_ID_BYTES = 128  # BM_COMM_ID_BYTES
+RUNS_TILED = 1  # BM_RUNS_TILED
 BM_OK, BM_E_ARG, BM_E_HIP, BM_E_WS, BM_E_COMM = 0, -1, -2, -3, -4
 
 _LIB = None

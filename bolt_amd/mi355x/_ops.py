@@ -257,14 +257,19 @@ class HipBackend(object):
             if (t.size == 0 or (ln <= 0).any() or (s0 < 0).any() or (s0 + ln > src_rec).any() or (a < 0).any()
                     or (m < 0).any() or (a + (group - 1) * m + ln > gstride).any()):
                 raise ValueError("record runs do not fit the records")
-            hit = (torch.from_numpy(t.reshape(-1).copy()).to(src.device), t.shape[0], int(vb))
+            t = t[np.argsort(t[:, 2], kind="stable")]
+            ends = t[:, 2] + int(group) * t[:, 1]
+            tiled = (t.shape[0] <= 64 and np.array_equal(t[:, 1], t[:, 3]) and t[0, 2] == 0 and
+                     np.array_equal(t[1:, 2], ends[:-1]) and ends[-1] * vb == int(gstride) * int(es))
+            hit = (torch.from_numpy(t.reshape(-1).copy()).to(src.device), t.shape[0], int(vb),
+                   _lib.RUNS_TILED if tiled else 0)
             if len(self._maps) >= 256:
                 self._drop_maps(src.device)
             self._maps[ck] = hit
-        table, n, vb = hit
+        table, n, vb, flags = hit
         _lib.check(self.lib.bm_record_runs(self._ptr(src, src_off), self._ptr(dst, dst_off), int(nrec), int(src_rec),
                                            int(group), int(gstride), int(n), ctypes.c_void_p(table.data_ptr()),
-                                           vb, int(es), self._stream(src)), "bm_record_runs")
+                                           vb, flags, int(es), self._stream(src)), "bm_record_runs")
 
     def _workspace(self, stat, code, O, R, I, device):
         import torch

@@ -532,8 +532,11 @@ class ChunkedArrayMI355X(object):
         ctx = self._ctx
         es = self._dtype.itemsize
         g = self._geom
-        per = g.size * int(np.prod(self._shape[1:self._split], dtype=np.int64)) * es
-        sizes = [(hi - lo) * per for lo, hi in ctx.bounds(self._shape[0])]
+        if ctx.world_size == 1:
+            sizes = [self._packed.numel()]
+        else:
+            per = g.size * int(np.prod(self._shape[1:self._split], dtype=np.int64)) * es
+            sizes = [(hi - lo) * per for lo, hi in ctx.bounds(self._shape[0])]
         host = gather_to_host(ctx, self._packed, sizes).view(self._dtype)
         kshape = self._shape[:self._split]
         ids = g.chunk_ids()

@@ -224,12 +224,18 @@ int bm_record_scatter(const void *src, void *dst, int64_t nrec, int64_t src_rec,
  * [elem_bytes, 16] dividing every record, stride and run; the caller checks
  * the runs lie inside the records and the destination).  src_rec and
  * dst_group_stride are in elements; nrec must be a multiple of group.
- * C5's keys_to_values((2,)): 16 chunk boxes of 2.6-3.2 KB per record, one
- * wave per box (bolt/spark/chunk.py:202-289).  Bit-exact.
+ * flags: BM_RUNS_TILED when the runs tile every new record (m_b = len_b and
+ * the regions [a_b, a_b + group * len_b), sorted by a_b, lie back to back
+ * from 0 to dst_group_stride; at most 64 runs): the kernel then walks the
+ * destination in order, whole lines per wave, each lane finding its source.
+ * C5's keys_to_values((2,)): 16 chunk boxes of 2.6-3.2 KB per record
+ * (bolt/spark/chunk.py:202-289).  Bit-exact.
  */
+#define BM_RUNS_TILED 1
 int bm_record_runs(const void *src, void *dst, int64_t nrec, int64_t src_rec,
                    int64_t group, int64_t dst_group_stride, int nruns,
-                   const int64_t *runs, int vec_bytes, int elem_bytes, void *stream);
+                   const int64_t *runs, int vec_bytes, int flags, int elem_bytes,
+                   void *stream);
 
 int bm_reduce_workspace_bytes(int stat, int in_dtype, int64_t O, int64_t R,
                               int64_t I, size_t *bytes);

@@ -38,7 +38,7 @@ def load(path):
     if hasattr(lib, "bm_record_runs"):
         lib.bm_record_runs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_void_p]
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     if hasattr(lib, "bm_record_gather_masked"):
         lib.bm_record_gather_masked.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                                 ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, I64P,
@@ -221,8 +221,10 @@ class RecRuns(object):
         map_a, map_b = plan.copies_to_scatter(plan.k2v_copies(g, new, [1, 1, 64], np.array([False, False, True])),
                                               64 * g.size, group=64, src_rec=g.size)
         runs, self.vb = plan.scatter_to_runs(map_a, map_b, g.size, new.size, 8)
+        runs = runs[np.argsort(runs[:, 2], kind="stable")]
         self.runs_host = runs * (self.vb // 8)
         self.n = runs.shape[0]
+        self.flags = int(os.environ.get("AB_RUNS_FLAGS", "1"))  # BM_RUNS_TILED (C5's boxes tile the records)
         self.table = torch.from_numpy(runs.reshape(-1).copy()).cuda()
         self.src = torch.randint(0, 255, (self.nrec * g.size * 8,), dtype=torch.uint8, device="cuda")
         self.dst = torch.empty(self.nrec // 64 * new.size * 8, dtype=torch.uint8, device="cuda")
@@ -231,7 +233,7 @@ class RecRuns(object):
     def __call__(self, lib):
         rc = lib.bm_record_runs(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.dst.data_ptr()),
                                 self.nrec, self.src_rec, self.group, self.gstride, self.n,
-                                ctypes.c_void_p(self.table.data_ptr()), self.vb, 8, stream())
+                                ctypes.c_void_p(self.table.data_ptr()), self.vb, self.flags, 8, stream())
         assert rc == 0, lib.bm_last_error()
 
     def check(self):
