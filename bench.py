@@ -1231,6 +1231,9 @@ def main():
         names = list(line["config"]["bytes_per_step"])
         recs = {names[0]: line["roofline"]}
         recs.update({n: v for n, v in line.get("stats_roofline", {}).items() if isinstance(v, dict)})
+        # every other op of the step: its traffic against its algorithmic bytes
+        line["ops_traffic"] = {n: {"bytes": int(line["config"]["bytes_per_step"][n])} for n in names if n not in recs}
+        recs.update(line["ops_traffic"])
         line["roofline"]["traffic_note"] = add_traffic(args.config, names, recs)
     if world == 1 and args.config == "C2" and not args.no_target64:
         # BASELINE.json's target sentence: swap and statistics of a 64 GiB

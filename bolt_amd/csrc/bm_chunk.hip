@@ -397,6 +397,9 @@ __global__ void __launch_bounds__(kCThreads)
 #ifndef BM_RUNS_DWALK_U
 #define BM_RUNS_DWALK_U 2
 #endif
+#ifndef BM_RUNS_XCD
+#define BM_RUNS_XCD 0  // XCD-contiguous destination eighths (A/B knob)
+#endif
 constexpr int kMaxWalkRuns = 64;
 template <int VB, int U>
 __global__ void __launch_bounds__(kCThreads)
@@ -413,7 +416,14 @@ __global__ void __launch_bounds__(kCThreads)
   const int lane = threadIdx.x & 63;
   const uint64_t per_block = (uint64_t)kCThreads * U;
   const uint64_t wave0 = (uint64_t)(threadIdx.x >> 6) * 64 * U;
-  for (uint64_t base = (uint64_t)blockIdx.x * per_block; base < total; base += (uint64_t)gridDim.x * per_block) {
+  const uint64_t nwork = (total + per_block - 1) / per_block;
+  // BM_RUNS_XCD: the blocks of one XCD (w % 8 under round-robin dispatch;
+  // the grid is a multiple of 8) take one contiguous eighth of the
+  // destination, so a source line shared by two boxes of a record is read
+  // again by the same XCD a region later, from its L2
+  const bool xcd = BM_RUNS_XCD && nwork % 8 == 0 && gridDim.x % 8 == 0;
+  for (uint64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const uint64_t base = (xcd ? (w % 8) * (nwork / 8) + w / 8 : w) * per_block;
     V x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
