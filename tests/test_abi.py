@@ -83,3 +83,25 @@ def test_workspace_and_state_sizes(lib):
     assert lib.bm_reduce_state_bytes(1, 10, 100, ctypes.byref(n)) == 0 and n.value == 1600
     assert lib.bm_reduce_state_bytes(0, 3, 100, ctypes.byref(n)) == 0 and n.value == 800
     assert lib.bm_reduce_state_bytes(3, 3, 100, ctypes.byref(n)) == 0 and n.value == 800
+
+
+def test_record_runs_argument_errors(lib):
+    """bm_record_runs refuses bad geometry before any launch: records not a
+    multiple of the group, vector widths that do not divide the record /
+    stride or exceed 16 B, a tiled walk with more than 64 runs, unknown flags,
+    null pointers; zero records is a no-op."""
+    from bolt_amd.mi355x import _lib
+    f = lib.bm_record_runs
+    assert f(None, None, 6, 64, 4, 256, 2, None, 16, 0, 8, None) == -1  # 6 records, group 4
+    assert b"bad arguments" in lib.bm_last_error()
+    assert f(None, None, 8, 63, 4, 256, 2, None, 16, 0, 8, None) == -1  # 63 f64 not a 16-B multiple
+    assert f(None, None, 8, 64, 4, 256, 2, None, 32, 0, 8, None) == -1  # 32-B vectors
+    assert f(None, None, 8, 64, 4, 256, 2, None, 4, 0, 8, None) == -1   # vector narrower than an element
+    assert f(None, None, 8, 64, 4, 256, 65, None, 16, _lib.RUNS_TILED, 8, None) == -1
+    assert f(None, None, 8, 64, 4, 256, 2, None, 16, 2, 8, None) == -1   # unknown flag
+    assert b"flags" in lib.bm_last_error()
+    assert f(None, None, 8, 64, 4, 256, 2, None, 16, 0, 8, None) == -1   # null pointers
+    assert b"null pointer" in lib.bm_last_error()
+    assert f(None, None, 0, 64, 4, 256, 2, None, 16, _lib.RUNS_TILED, 8, None) == 0  # nothing to move
+    rc = lib.bm_record_scatter(None, None, 4, 64, 4, 256, None, None, 3, 8, None)  # vec not a power of two
+    assert rc == -1 and b"bad arguments" in lib.bm_last_error()
