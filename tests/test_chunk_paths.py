@@ -288,3 +288,51 @@ def test_scatter_to_runs_table():
     assert scatter_to_runs(un[0], un[1], g.size, 64 * 64, 8) is None
     a = np.arange(1089, dtype=np.int32)
     assert scatter_to_runs(a, np.zeros_like(a), 1089, 1089, 1)[1] == 1
+
+
+def _runs_fuzz_cases(n=24, seed=21):
+    """Random keys_to_values geometries of the trailing key whose scatter plan
+    bm_record_runs takes (plan.scatter_to_runs: few runs of >= 1 KiB on
+    average), every element size."""
+    from bolt_amd.mi355x.plan import ChunkGeometry, copies_to_scatter, k2v_copies, scatter_to_runs
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        dt = [np.uint8, np.int16, np.float32, np.float64][int(rng.integers(0, 4))]
+        es = np.dtype(dt).itemsize
+        nv = int(rng.integers(1, 3))
+        vshape = tuple(int(v) for v in rng.integers(8, 72, nv))
+        plan = tuple(int(rng.integers(max(2, v // 4), v + 1)) for v in vshape)
+        pad = tuple(int(rng.integers(0, min(3, v - p) + 1)) if p < v else 0 for p, v in zip(plan, vshape))
+        if np.prod(vshape) * es > 40000:
+            continue
+        split = int(rng.integers(1, 3))
+        kshape = tuple(int(k) for k in rng.integers(1, 4, split - 1)) + (int(rng.integers(2, 6)),)
+        K = kshape[-1]
+        g = ChunkGeometry(vshape, plan, pad)
+        new = ChunkGeometry((K,) + vshape, (K,) + plan, (0,) + pad)
+        sc = copies_to_scatter(k2v_copies(g, new, [1] * (split - 1) + [K], np.array([False] * (split - 1) + [True])),
+                               K * g.size, group=K, src_rec=g.size)
+        if sc is None or scatter_to_runs(sc[0], sc[1], g.size, new.size, es) is None:
+            continue
+        out.append((kshape + vshape, split, dt, plan, pad))
+    return out
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_record_runs_fuzz(bctx, monkeypatch, case):
+    """Seeded random geometries: keys_to_values of the trailing key through the
+    runs kernel (destination walk when the boxes tile the new records) equals
+    the strided-copy path, and its unchunk restores the input."""
+    shape, split, dtype, plan, pad = _runs_fuzz_cases()[case]
+    rng = np.random.default_rng(case)
+    x = rng.integers(0, 250, size=shape).astype(dtype)
+    out = {}
+    for runs, scatter in (("1", "1"), ("0", "0")):
+        monkeypatch.setenv("BOLT_AMD_RUNS", runs)
+        monkeypatch.setenv("BOLT_AMD_SCATTER", scatter)
+        c = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad)
+        k = c.keys_to_values((split - 1,))
+        out[runs] = (k._packed.cpu().numpy().tobytes(), k.unchunk().toarray().tobytes(), k.plan.tolist(),
+                     k.padding.tolist(), k.shape)
+    assert out["1"] == out["0"], (shape, split, dtype, plan, pad)
