@@ -18,8 +18,9 @@ runs on; `stats_roofline` the same for the reduction kernels of mean / std;
 Sub-records of the default run (same JSON line; `value` stays C2's):
   target64  BASELINE.json's target, swap + mean/std of a 64 GiB float32 4-D
             array (1 GPU only);
-  configs   C3, C4 and C5 (BASELINE configs[2..4]), a few steps each: value,
-            per-op hipEvents time, fraction of HBM peak and PMC traffic.
+  configs   C1, C3, C4 and C5 (BASELINE configs[0], [2..4]), a few steps
+            each: value, per-op hipEvents time, fraction of HBM peak and PMC
+            traffic.
 `checks` compares the results of every permute (bit for bit) and of every
 statistic over the sharded axis (float64 truth, stated tolerance) with the
 global array rebuilt from each rank's seed; `cpu_baseline` times the oracle's
@@ -68,7 +69,7 @@ CONFIGS = {
     "target64": ((8192, 256, 256, 32), np.float32, 2,
                  "64 GiB float32 4-D per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
 }
-SUB_CONFIGS = ("C3", "C4", "C5")  # sub-records of the default run
+SUB_CONFIGS = ("C1", "C3", "C4", "C5")  # sub-records of the default run
 
 
 def parse(argv=None):
@@ -86,7 +87,7 @@ def parse(argv=None):
                     help="skip the 64 GiB north_star sub-record of the default (C2, 1 GPU) run")
     ap.add_argument("--target-steps", type=int, default=5)
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the C3/C4/C5 sub-records of the default (C2) run")
+                    help="skip the C1/C3/C4/C5 sub-records of the default (C2) run")
     ap.add_argument("--config-steps", type=int, default=3)
     ap.add_argument("--no-checks", action="store_true", help="skip the post-timing result checks")
     # internal: rocprofv3 child, CPU-baseline child, rehearsal shapes (JSON {config: per-rank shape})

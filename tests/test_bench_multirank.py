@@ -168,8 +168,8 @@ def test_stat_checks_catch_a_wrong_result(monkeypatch):
     del torch
 
 
-SHAPES = json.dumps({"C2": [4, 8, 8], "C3": [2, 3, 4, 8], "C4": [6, 16, 16], "C5": [2, 2, 2, 20, 20],
-                     "target64": [2, 3, 4, 8]})
+SHAPES = json.dumps({"C1": [5, 6, 4], "C2": [4, 8, 8], "C3": [2, 3, 4, 8], "C4": [6, 16, 16],
+                     "C5": [2, 2, 2, 20, 20], "target64": [2, 3, 4, 8]})
 
 
 def _bench(args, env_extra, timeout=600):
@@ -197,11 +197,13 @@ def test_bench_launches_its_ranks(world):
     assert d["n_gpus"] == world and d["launcher"].startswith("bench.py --gpus %d" % world)
     assert d["exchange_check"] == "bit-exact"
     assert d["config"]["global_shape"][0] == 4 * world
-    for cfg in ("C3", "C4", "C5"):
+    for cfg in ("C1", "C3", "C4", "C5"):
         c = d["configs"][cfg]
         assert c["checks"]["all"].startswith("every result matches"), (cfg, c["checks"])
         assert c["global_shape"][0] == json.loads(SHAPES)[cfg][0] * world
     assert d["configs"]["C4"]["checks"]["var"].startswith("within rtol 1e-12")
+    assert all(d["configs"]["C1"]["checks"][n].startswith("within rtol 1e-12")
+               for n in ("sum_all", "mean_0", "var_all", "std_0"))  # C1's stats reduce the sharded axis
     assert "target64" not in d  # the 64 GiB target is a one-GPU record
 
 
@@ -216,7 +218,7 @@ def test_bench_refuses_gpu_count_mismatch():
 
 def test_bench_one_rank_rehearsal_record():
     """The default run's record on one rank (CPU rehearsal): the headline line,
-    stats_roofline for mean / std, target64 and the C3 / C4 / C5 sub-records
+    stats_roofline for mean / std, target64 and the C1 / C3 / C4 / C5 sub-records
     with per-op time and fraction of peak, and the checks."""
     r = _bench(["--steps", "2", "--warmup", "1", "--no-pmc", "--no-cpu-baseline", "--target-steps", "1",
                 "--shard-shapes", SHAPES], {"BOLT_AMD_BENCH_DEVICE": "cpu"})
