@@ -398,7 +398,15 @@ __global__ void __launch_bounds__(kCThreads)
 #define BM_RUNS_DWALK_U 2
 #endif
 #ifndef BM_RUNS_XCD
-#define BM_RUNS_XCD 0  // XCD-contiguous destination eighths (A/B knob)
+// 1: the blocks of one XCD walk one contiguous eighth of the destination.
+// With temporal source loads (BM_RUNS_TLOAD) a source line that two chunk
+// boxes of a record share is then read again a region later from the same
+// XCD's L2: PMC traffic 1.0375x -> 1.0000x and +0.7..+2.5% on C5's
+// keys_to_values (profiles/r04o_runs_xcd.log)
+#define BM_RUNS_XCD 1
+#endif
+#ifndef BM_RUNS_TLOAD
+#define BM_RUNS_TLOAD 1  // destination walk: temporal source loads (0: non-temporal, A/B knob)
 #endif
 constexpr int kMaxWalkRuns = 64;
 template <int VB, int U>
@@ -419,8 +427,7 @@ __global__ void __launch_bounds__(kCThreads)
   const uint64_t nwork = (total + per_block - 1) / per_block;
   // BM_RUNS_XCD: the blocks of one XCD (w % 8 under round-robin dispatch;
   // the grid is a multiple of 8) take one contiguous eighth of the
-  // destination, so a source line shared by two boxes of a record is read
-  // again by the same XCD a region later, from its L2
+  // destination (affinity only: any block-to-XCD mapping is correct)
   const bool xcd = BM_RUNS_XCD && nwork % 8 == 0 && gridDim.x % 8 == 0;
   for (uint64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
     const uint64_t base = (xcd ? (w % 8) * (nwork / 8) + w / 8 : w) * per_block;
@@ -441,7 +448,8 @@ __global__ void __launch_bounds__(kCThreads)
         int64_t k = (int64_t)((double)off * inv[lo]);
         if (k * len > off) --k;
         else if ((k + 1) * len <= off) ++k;
-        x[u] = ld_src(s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + (off - k * len));
+        const V *sp = s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + (off - k * len);
+        x[u] = BM_RUNS_TLOAD ? *sp : ld_src(sp);
       }
     }
 #pragma unroll
