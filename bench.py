@@ -1155,6 +1155,23 @@ def main():
                             "achieved": round(nb / (ms / 1e3) / 1e9, 1),
                             "frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None}
             line["stats_roofline"] = sr
+        if world == 1 and not args.pmc_child:
+            # every op's own library launches, in K more steps (per-op detail of
+            # the step; outside the timed region for the same reason)
+            clock = KernelClock(be, dev, LAUNCHES, pool=steps * len(ops) * 4)
+            try:
+                timed_steps(ops, steps, clock=clock)
+            finally:
+                clock.close()
+            line["ops"] = {}
+            for name, _, nb in ops:
+                ms = clock.ms(name, steps)
+                o = {"bytes": int(nb), "ms": round(ms, 4) if ms else None,
+                     "launches_per_call": clock.launches(name, steps)}
+                if ms and nb:
+                    o["achieved"] = round(nb / (ms / 1e3) / 1e9, 1)
+                    o["frac"] = round(o["achieved"] / HBM_PEAK_GBPS, 4)
+                line["ops"][name] = o
         line["checks"] = checks(cfg, b, shape, dtype)
         if world > 1:
             line["exchange_check"] = (line["checks"] or {}).get(ops[0][0])
@@ -1233,9 +1250,14 @@ def main():
         recs = {names[0]: line["roofline"]}
         recs.update({n: v for n, v in line.get("stats_roofline", {}).items() if isinstance(v, dict)})
         # every other op of the step: its traffic against its algorithmic bytes
-        line["ops_traffic"] = {n: {"bytes": int(line["config"]["bytes_per_step"][n])} for n in names if n not in recs}
-        recs.update(line["ops_traffic"])
+        recs.update({n: o for n, o in line.get("ops", {}).items() if n not in recs})
         line["roofline"]["traffic_note"] = add_traffic(args.config, names, recs)
+        for n, o in line.get("ops", {}).items():
+            src = recs.get(n)
+            if src is not o and src is not None and "traffic" in src:
+                o["traffic"] = src["traffic"]
+                if "traffic_ratio" in src:
+                    o["traffic_ratio"] = src["traffic_ratio"]
     if world == 1 and args.config == "C2" and not args.no_target64:
         # BASELINE.json's target sentence: swap and statistics of a 64 GiB
         # float32 4-D array on one GPU at >= 60% of the HBM roofline
