@@ -224,6 +224,15 @@ def test_bench_one_rank_rehearsal_record():
                 "--shard-shapes", SHAPES], {"BOLT_AMD_BENCH_DEVICE": "cpu"})
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
+    # the driver's contract: one JSON line with these keys
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert d["unit"] == "GB/s" and d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "f32"
+    assert set(d["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
+    assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
+    assert set(d["ops"]) == {"swap", "mean", "std"} and all(o["bytes"] > 0 for o in d["ops"].values())
     assert d["n_gpus"] == 1 and set(d["stats_roofline"]) >= {"mean", "std"}
     assert d["stats_roofline"]["mean"]["launches_per_call"] == 1.0
     assert d["checks"]["swap"] == "bit-exact"
