@@ -55,20 +55,6 @@ constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane 
 #ifndef BM_INT_UNROLL
 #define BM_INT_UNROLL 8  // exact-integer column var: rows in flight per lane (C4 var 3.76 -> 3.47 ms over 4, profiles/r02_ab_int.log)
 #endif
-#ifndef BM_RED_ROWS_TLOAD
-#define BM_RED_ROWS_TLOAD 0  // rows kernel: temporal loads, so a line two neighbouring rows share stays in L2 (A/B knob)
-#endif
-template <typename T, int N>
-__device__ __forceinline__ void vload_rows(const T *p, T (&out)[N]) {
-  if (BM_RED_ROWS_TLOAD) {
-    typedef typename VecB<N * sizeof(T)>::t V;
-    const V v = *reinterpret_cast<const V *>(p);
-    __builtin_memcpy(out, &v, sizeof(V));
-  } else {
-    vload_nt<T, N>(p, out);
-  }
-}
-
 #ifndef BM_RED_XCD
 #define BM_RED_XCD 1  // rows kernel: blocks dealt to one XCD take consecutive rows (C2 mean / std +3-4%, profiles/r02_ab_redxcd.log)
 #endif
@@ -656,7 +642,7 @@ __global__ void __launch_bounds__(kThreads)
   for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
     T v[kRowsUnroll][VEC];
 #pragma unroll
-    for (int u = 0; u < kRowsUnroll; ++u) vload_rows<T, VEC>(row + j + u * stride, v[u]);
+    for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
     if constexpr (MODE == M_MOM) {
       // the kRowsUnroll * VEC values in hand form one Welford batch
       double x[kRowsUnroll * VEC];
@@ -691,7 +677,7 @@ __global__ void __launch_bounds__(kThreads)
   for (; j < r_hi; j += stride) {
     if (j + VEC <= r_hi) {
       T v[VEC];
-      vload_rows<T, VEC>(row + j, v);
+      vload_nt<T, VEC>(row + j, v);
       if constexpr (MODE == M_MOM) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
