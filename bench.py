@@ -481,6 +481,26 @@ def exchange_check(torch, cfg, b, ctx, dev, shape=None, dtype=None, split=None):
 
 # ------------------------------------------------------------ PMC traffic --
 
+def run_child(cmd, timeout, capture=False):
+    """Run ``cmd`` in its own process group and return (rc, stdout bytes); on
+    timeout the whole group is killed (a profiler's or a worker pool's
+    grandchildren included), and the rc is -9."""
+    import signal
+    import subprocess
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE if capture else subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout)
+        return p.returncode, out or b""
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.communicate()
+        return -9, b""
+
+
 def _library_kernel(name):
     import re
     return re.search(r"(?<![A-Za-z0-9_])k_(transpose|rowcopy|generic|red|recmap|record|gather)", name) is not None
@@ -501,7 +521,6 @@ def pmc_traffic(cfg, args, nops, warmup=1, steps=2):
     import csv
     import glob
     import shutil
-    import subprocess
     import tempfile
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
@@ -515,10 +534,12 @@ def pmc_traffic(cfg, args, nops, warmup=1, steps=2):
         if args.shard_shapes:
             cmd += ["--shard-shapes", args.shard_shapes]
         try:
-            subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600, check=True)
-        except Exception as e:  # profiler unavailable or refused: report null
+            rc, _ = run_child(cmd, timeout=600)
+        except OSError as e:  # profiler unavailable: report null
+            rc = "%s" % type(e).__name__
+        if rc != 0:
             shutil.rmtree(out, ignore_errors=True)
-            return None, "rocprofv3 --pmc %s failed: %s" % (ctr, type(e).__name__)
+            return None, "rocprofv3 --pmc %s failed: %s" % (ctr, rc)
         disp = {}  # dispatch id -> [kernel name, counter value in bytes]
         for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
@@ -797,17 +818,18 @@ def cpu_baseline_in_child(args, cfg):
     """cpu_baseline() in a fresh child process of this script that never
     touches the GPU (its local[8] analogue forks workers: never from a process
     with a live HIP runtime)."""
-    import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", cfg]
     if args.cpu_sample_rows:
         cmd += ["--cpu-sample-rows", str(args.cpu_sample_rows)]
     if args.shard_shapes:
         cmd += ["--shard-shapes", args.shard_shapes]
+    rc, out = run_child(cmd, timeout=900, capture=True)
     try:
-        p = subprocess.run(cmd, stdout=subprocess.PIPE, timeout=900, check=True)
-        return json.loads(p.stdout.decode().strip().splitlines()[-1])
-    except Exception as e:
-        return {"value": None, "note": "CPU baseline child failed: %s" % type(e).__name__}
+        if rc != 0:
+            raise RuntimeError("exit status %d" % rc)
+        return json.loads(out.decode().strip().splitlines()[-1])
+    except (RuntimeError, ValueError, IndexError) as e:
+        return {"value": None, "note": "CPU baseline child failed: %s" % e}
 
 
 # ------------------------------------------------------------------ timing --
