@@ -6,7 +6,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 T=${TAG:-r04g}
-SHAPES='{"C1":[100,64,64],"C2":[200,512,512],"C3":[64,256,256,32],"C4":[200,1024,1024],"C5":[4,64,64,64,64]}'
+SHAPES=${SHAPES:-'{"C1":[100,64,64],"C2":[200,512,512],"C3":[64,256,256,32],"C4":[200,1024,1024],"C5":[4,64,64,64,64]}'}
 for n in ${NS:-2 4}; do
   echo "[$(date +%T)] $n ranks"
   BOLT_AMD_BENCH_BACKEND=gloo BOLT_AMD_BENCH_DEVICE=0 timeout -k 10 600 python bench.py --gpus $n --steps 3 --warmup 1 --shard-shapes "$SHAPES" > gpurun_out/${T}_n${n}_rehearsal.json 2> gpurun_out/${T}_n${n}_rehearsal.err || { echo REHEARSAL_FAIL $n; tail -30 gpurun_out/${T}_n${n}_rehearsal.err; exit 1; }
