@@ -9,7 +9,7 @@
 //   cols kernel (I > 1): lanes own VEC adjacent columns, 16-B loads along I,
 //     row phases stride R; phases are Chan-combined through LDS.
 //   rows kernel (I == 1): one wave per (row, chunk), 16-B loads along R,
-//     Chan combination across the 64 lanes by __shfl_xor.
+//     lane states folded across the 64 lanes through DPP moves (wave_fold).
 //   Long R is split into chunks over blocks (enough waves to fill 256 CUs);
 //   chunk states go to a workspace and a combine kernel merges them in chunk
 //   order (deterministic) and finalises.
@@ -105,6 +105,50 @@ template <typename T> __device__ __forceinline__ T from_bits(uint64_t u) {
   return x;
 }
 template <typename T> __device__ __forceinline__ bool is_nan(T x) { return x != x; }
+
+// ---- wave fold through DPP ----
+// A 64-bit lane value moved by a DPP modifier of v_mov (two 32-bit halves, the
+// same source lane): the cross-lane read stays in the VALU, no LDS round trip
+// as __shfl_xor's ds_bpermute takes.  Controls (GFX9 DPP): quad_perm [1,0,3,2]
+// = 0xB1 (lane ^ 1), [2,3,0,1] = 0x4E (lane ^ 2), row_half_mirror 0x141
+// (lane 7-i of its 8), row_mirror 0x140 (lane 15-i of its row), row_bcast15
+// 0x142 (lane 15 of row r -> row r+1), row_bcast31 0x143 (lane 31 -> rows 2, 3).
+template <int CTRL, typename V> __device__ __forceinline__ V dpp_mov(V v) {
+  static_assert(sizeof(V) == 8, "64-bit lane values");
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(V, ((uint64_t)hi << 32) | lo);
+}
+// Lane 63 receives op over all 64 lanes, combined in lane order: every step
+// combines (lower lanes, upper lanes), so the result equals a left fold over
+// lanes 0..63 for any associative op (first NaN / first of equal values wins,
+// as in a sequential scan).  Steps 1-4 leave identical bits in the lanes that
+// feed the next step (both lanes of a pair form op(lower, upper)); steps 5-6
+// fold the four 16-lane rows.  Requires all 64 lanes active.
+template <typename V, typename F> __device__ __forceinline__ V wave_fold(V v, int lane, F op) {
+  V p = dpp_mov<0xB1>(v);
+  v = (lane & 1) ? op(p, v) : op(v, p);
+  p = dpp_mov<0x4E>(v);
+  v = (lane & 2) ? op(p, v) : op(v, p);
+  p = dpp_mov<0x141>(v);
+  v = (lane & 4) ? op(p, v) : op(v, p);
+  p = dpp_mov<0x140>(v);
+  v = (lane & 8) ? op(p, v) : op(v, p);
+  p = dpp_mov<0x142>(v);
+  if (lane & 16) v = op(p, v);  // lane 31 = rows 0+1, lane 63 = rows 2+3
+  p = dpp_mov<0x143>(v);
+  if (lane & 32) v = op(p, v);  // lane 63 = (rows 0+1) + (rows 2+3)
+  return v;
+}
+constexpr int kFoldLane = 63;
+// lane 0's value in every lane (v_readlane into a scalar register)
+__device__ __forceinline__ double lane0_of(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 0);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 0);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 
 // numpy.maximum / numpy.minimum: a NaN operand wins (NaNs propagate)
 template <typename T, bool MAX> __device__ __forceinline__ T pick(T a, T b) {
@@ -672,7 +716,7 @@ __global__ void __launch_bounds__(kThreads)
   // around one wave-wide pivot C = lane 0's Welford mean (lane 0 holds 1/64
   // of the main-loop data, so n (mean - C)^2 <= 64 M2 and S2 - S1^2/n loses
   // at most ~6 bits): plain adds, no division per lane or per butterfly step
-  const double C = (MODE == M_MOM) ? __shfl(w.mean, 0) : 0.0;
+  const double C = (MODE == M_MOM) ? lane0_of(w.mean) : 0.0;
   double t1 = 0.0, t2 = 0.0;
   for (; j < r_hi; j += stride) {
     if (j + VEC <= r_hi) {
@@ -706,10 +750,9 @@ __global__ void __launch_bounds__(kThreads)
     }
   }
 
-  // wave combination (butterfly, fixed order -> deterministic).  Both lanes
-  // of a pair combine (lower lane, upper lane) in that order, so they hold
-  // identical bits afterwards.  mean: shared pivot, the S1 sums simply add;
-  // var / std: each lane's Welford state as sums around C, which add.
+  // wave combination: DPP fold into lane 63 in lane order (deterministic).
+  // mean: shared pivot, the S1 sums simply add; var / std: each lane's
+  // Welford state as sums around C, which add.
   double m = facc_mode<MODE>() ? fs : acc.s1();
   double wq = 0.0;
   if constexpr (MODE == M_MOM) {
@@ -717,23 +760,15 @@ __global__ void __launch_bounds__(kThreads)
     const double s1 = w.n * dm;
     m = s1 + t1;
     wq = fma(s1, dm, w.m2) + t2;
+    const auto add = [](double a, double b) { return a + b; };
+    m = wave_fold(m, lane, add);
+    wq = wave_fold(wq, lane, add);
+  } else if constexpr (MODE == M_MEAN || facc_mode<MODE>()) {
+    m = wave_fold(m, lane, [](double a, double b) { return fop<MODE>(a, b); });
+  } else {
+    us = wave_fold(us, lane, [](uint64_t a, uint64_t b) { return bop<T, MODE>(a, b); });
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    if (MODE == M_MOM) {
-      const double mb = __shfl_xor(m, off), qb = __shfl_xor(wq, off);
-      m = (lane & off) ? (mb + m) : (m + mb);
-      wq = (lane & off) ? (qb + wq) : (wq + qb);
-    } else if (MODE == M_MEAN || facc_mode<MODE>()) {
-      const double mb = __shfl_xor(m, off);
-      // lower lane combines (self, partner), upper lane (partner, self)
-      m = (lane & off) ? fop<MODE>(mb, m) : fop<MODE>(m, mb);
-    } else {
-      const uint64_t ub = (uint64_t)__shfl_xor((long long)us, off);
-      us = (lane & off) ? bop<T, MODE>(ub, us) : bop<T, MODE>(us, ub);
-    }
-  }
-  if (lane != 0) return;
+  if (lane != kFoldLane) return;
   const double ntot = (double)(r_hi - r_lo);
   const int64_t e = (int64_t)o;
   const int64_t idx = sk.final_out ? e : (c * d.O + e);
@@ -924,12 +959,10 @@ __global__ void __launch_bounds__(kThreads)
       }
     }
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    s1 += (int64_t)__shfl_xor((long long)s1, off);
-    s2 += (uint64_t)__shfl_xor((long long)s2, off);
-  }
-  if (lane != 0) return;
+  // exact integer sums: any order gives the same bits
+  s1 = wave_fold(s1, lane, [](int64_t a, int64_t b) { return a + b; });
+  s2 = wave_fold(s2, lane, [](uint64_t a, uint64_t b) { return a + b; });
+  if (lane != kFoldLane) return;
   const int64_t n = r_hi - r_lo;
   const int64_t e = (int64_t)o;
   const int64_t idx = sk.final_out ? e : (c * d.O + e);
