@@ -13,27 +13,33 @@ the host as the reference does.
 ranks), GB/s:  swap 2*N*s, each stat N*s + outputs.  `roofline` is the
 dominant kernel (the swap's permute) measured with hipEvents on the stream it
 runs on; `stats_roofline` the same for the reduction kernels of mean / std;
-`traffic` comes from rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE).
+traffic comes from rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE).
 
 Sub-records of the default run (same JSON line; `value` stays C2's):
+  configs   C1, C3, C4 and C5 (BASELINE configs[0], [2..4]) on their GLOBAL
+            shapes (strong scaling: N slabs of the leading axis), a few steps
+            each: value, per-op time, fraction of HBM peak, PMC traffic;
   target64  BASELINE.json's target, swap + mean/std of a 64 GiB float32 4-D
-            array (1 GPU only);
-  configs   C1, C3, C4 and C5 (BASELINE configs[0], [2..4]), a few steps
-            each: value, per-op hipEvents time, fraction of HBM peak and PMC
-            traffic.
-`checks` compares the results of every permute (bit for bit) and of every
-statistic over the sharded axis (float64 truth, stated tolerance) with the
-global array rebuilt from each rank's seed; `cpu_baseline` times the oracle's
-restatement of the reference Spark path and the local mode's numpy calls in a
-child process that never touches the GPU.
+            array (1 GPU only).
+Every op of every step is checked after timing (`ck`): permutes, chunk /
+unchunk / keys_to_values / values_to_keys bit for bit against torch on the
+global array rebuilt from each rank's seed, statistics against a float64
+truth at the stated tolerance.  `cpu_baseline` times the oracle's restatement
+of the reference Spark path and the local mode's numpy calls in a child
+process that never touches the GPU.
+
+The line holds numbers and short codes only (profiles/BENCH_FIELDS.md is the
+legend), ordered so that the driver's kept tail holds every sub-record; the
+prose goes to the detail file named in `detail`.
 
 N GPUs: `python bench.py --gpus N` starts the N rank processes itself (one
 per GPU, before anything touches the GPU; rank 0's JSON line is relayed), or
 runs as one rank of `torch.distributed.run --nproc-per-node N ... --gpus N`.
 A --gpus that differs from WORLD_SIZE, or more GPUs than are visible, exits 2.
-Weak scaling: the leading axis grows with N, the swap becomes pack ->
-all-to-all -> unpack over RCCL, sharded-axis statistics all_gather their
-partial states.
+The headline scales weakly (the leading axis grows with N); the swap becomes
+pack -> all-to-all -> unpack over RCCL, sharded-axis statistics all_gather
+their partial states.  Rank 0 runs under rocprofv3 --kernel-trace --stats
+(rocprof_rank0) and a marked pass attributes its kernels to op calls.
 """
 import argparse
 import json
@@ -52,22 +58,23 @@ XGMI_LINK_GBPS = 153.0      # per link, per direction
 METRIC = "swap/transpose GB/s + stat-reduce GB/s, % of HBM/xGMI roofline, 1-8 GPUs"
 
 CONFIGS = {
-    # name: (per-GPU shape, dtype, split, description)
-    "C1": ((100, 64, 64), np.float64, 1,
-           "C1: float64 (100,64,64), key 0; swap((0,),(0,)) then sum/mean/var/std at axis=None and "
-           "axis=(0,) of the swapped array (the reference's CPU-runnable case)"),
-    "C2": ((2000, 512, 512), np.float32, 1,
-           "C2: float32 (2000,512,512) per GPU, key=time; swap((0,),(0,1)) + mean/std over time"),
-    "C3": ((4096, 256, 256, 32), np.float32, 2,
-           "C3: float32 (4096,256,256,32) per GPU, keys (0,1); swap((0,),(0,)) + .T"),
-    "C4": ((10000, 1024, 1024), np.uint16, 1,
-           "C4: uint16 (10000,1024,1024) per GPU, key 0; swap((0,),(0,)) + chunk('150') -> unchunk "
-           "(plan (73, 1024): the packed layout is the dense one, no bytes move) + float64 var over axis 0"),
-    "C5": ((64, 64, 64, 64, 64), np.float64, 3,
-           "C5: float64 64^5 per GPU, keys (0,1,2); .T + transpose(2,0,4,1,3) + "
-           "chunk((16,16), padding=2) -> unchunk / keys_to_values((2,)) / values_to_keys((0,))"),
-    "target64": ((8192, 256, 256, 32), np.float32, 2,
-                 "64 GiB float32 4-D per GPU, keys (0,1); swap((0,),(0,)) + mean/std over axis 0"),
+    # name: (shape, dtype, split, scaling, short workload code)
+    #   weak:   ``shape`` is one rank's slab; the global leading axis is shape[0] * N
+    #   strong: ``shape`` is BASELINE.json's global array, cut into N slabs of
+    #           its leading axis (construct.py:66-69 partitions a fixed array)
+    "C1": ((100, 64, 64), np.float64, 1, "strong",
+           "C1 f64 (100,64,64) key 0: swap((0,),(0,)) + sum/mean/var/std at axis None and (0,)"),
+    "C2": ((2000, 512, 512), np.float32, 1, "weak",
+           "C2 f32 (2000,512,512)/GPU key=time: swap((0,),(0,1)) + mean/std(axis=2)"),
+    "C3": ((4096, 256, 256, 32), np.float32, 2, "strong",
+           "C3 f32 (4096,256,256,32) keys (0,1): swap((0,),(0,)) + .T"),
+    "C4": ((10000, 1024, 1024), np.uint16, 1, "strong",
+           "C4 u16 (10000,1024,1024) key 0: swap((0,),(0,)) + chunk('150') -> unchunk + var(axis=0)"),
+    "C5": ((64, 64, 64, 64, 64), np.float64, 3, "strong",
+           "C5 f64 64^5 keys (0,1,2): .T + transpose(2,0,4,1,3) + chunk((16,16),pad 2) -> unchunk / "
+           "keys_to_values((2,)) / values_to_keys((0,))"),
+    "target64": ((8192, 256, 256, 32), np.float32, 2, "weak",
+                 "target64 f32 (8192,256,256,32)=64 GiB/GPU keys (0,1): swap((0,),(0,)) + mean/std(axis=0)"),
 }
 SUB_CONFIGS = ("C1", "C3", "C4", "C5")  # sub-records of the default run
 
@@ -83,6 +90,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
+    ap.add_argument("--no-rocprof", action="store_true",
+                    help="N > 1: do not run rank 0 under rocprofv3 --kernel-trace --stats")
     ap.add_argument("--no-target64", action="store_true",
                     help="skip the 64 GiB north_star sub-record of the default (C2, 1 GPU) run")
     ap.add_argument("--target-steps", type=int, default=5)
@@ -90,23 +99,34 @@ def parse(argv=None):
                     help="skip the C1/C3/C4/C5 sub-records of the default (C2) run")
     ap.add_argument("--config-steps", type=int, default=3)
     ap.add_argument("--no-checks", action="store_true", help="skip the post-timing result checks")
-    # internal: rocprofv3 child, CPU-baseline child, rehearsal shapes (JSON {config: per-rank shape})
+    ap.add_argument("--detail", default=None,
+                    help="file for the full record with its prose (default gpurun_out/bench_detail_n<N>.json)")
+    # internal: rocprofv3 child, CPU-baseline child, rehearsal shapes (JSON {config: shape}: a weak
+    # config's per-rank slab, a strong config's global array)
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--shard-shapes", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--shapes", "--shard-shapes", dest="shapes", default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
-def config_of(args, cfg):
-    """(per-rank shape, dtype, split, description) of a config; --shard-shapes
-    (rehearsals on small data) overrides the shape."""
-    shape, dtype, split, desc = CONFIGS[cfg]
-    if args.shard_shapes:
-        over = json.loads(args.shard_shapes)
+def config_of(args, cfg, world=1):
+    """(global shape, dtype, split, scaling, workload code) of a config at
+    ``world`` ranks; --shapes (rehearsals on small data) overrides the shape."""
+    shape, dtype, split, scaling, desc = CONFIGS[cfg]
+    if args.shapes:
+        over = json.loads(args.shapes)
         if cfg in over:
             shape = tuple(int(s) for s in over[cfg])
-            desc = "REHEARSAL SHAPE %s -- %s" % (str(shape), desc)
-    return shape, dtype, split, desc
+            desc = "REHEARSAL %s: %s" % (str(shape).replace(" ", ""), desc)
+    if scaling == "weak":
+        shape = (shape[0] * world,) + tuple(shape[1:])
+    return tuple(shape), dtype, split, scaling, desc
+
+
+def slab_shapes(gshape, world):
+    """Every rank's slab shape of a global array (MI355XContext.bounds: array_split order)."""
+    base, extra = divmod(int(gshape[0]), world)
+    return [(base + (1 if r < extra else 0),) + tuple(gshape[1:]) for r in range(world)]
 
 
 # ----------------------------------------------------------------- launcher --
@@ -278,14 +298,20 @@ def steps_of(cfg, b, world=1):
 # ------------------------------------------------------------------ checks --
 
 def checks_of(cfg, b):
-    """The results the bench checks after timing, as (name, call, spec):
-    spec ("perm", perm) -- the call returns x.transpose(perm), compared bit for
-    bit; spec ("stat", name, axis, pre) -- a statistic over ``axis`` of
-    x.transpose(pre) (pre None: of x) that reduces the sharded leading axis
-    (reduce_state -> all_gather -> ordered Chan combine across GPUs)."""
-    from bolt_amd.mi355x.plan import swap_perm
+    """One check per op of the config's step (steps_of), as (name, call, spec):
+      ("perm", perm)             the call returns x.transpose(perm): bit for bit;
+      ("stat", name, axis, pre)  a statistic over ``axis`` of x.transpose(pre)
+                                 (pre None: of x) against a float64 truth;
+      ("packed", vshape, plan, pad)  the call returns a chunked array whose
+                                 records are x.reshape(-1, *vshape): its packed
+                                 buffer against the reference's slice rule
+                                 (chunk.py:574-618) applied with torch slicing,
+                                 and its plan / padding.
+    x is the global array rebuilt from every rank's seed."""
+    from bolt_amd.mi355x.plan import swap_perm, getplan
     nd = len(b.shape)
     rev = list(range(nd))[::-1]
+    ident = list(range(nd))
     if cfg == "C1":
         p = swap_perm(nd, b.split, (0,), (0,))[0]
         out = [("swap", lambda: b.swap((0,), (0,)), ("perm", p))]
@@ -296,16 +322,32 @@ def checks_of(cfg, b):
                             ("stat", name, ax, p)))
         return out
     if cfg == "C2":
-        return [("swap", lambda: b.swap((0,), (0, 1)), ("perm", swap_perm(nd, b.split, (0,), (0, 1))[0]))]
+        # mean / std over time (axis 2) of the swapped array = over axis 0 of x
+        return [("swap", lambda: b.swap((0,), (0, 1)), ("perm", swap_perm(nd, b.split, (0,), (0, 1))[0])),
+                ("mean", lambda: b.swap((0,), (0, 1)).mean(axis=2), ("stat", "mean", (0,), None)),
+                ("std", lambda: b.swap((0,), (0, 1)).std(axis=2), ("stat", "std", (0,), None))]
     if cfg == "C3":
         return [("swap", lambda: b.swap((0,), (0,)), ("perm", swap_perm(nd, b.split, (0,), (0,))[0])),
                 ("T", lambda: b.T, ("perm", rev))]
     if cfg == "C4":
+        vshape = tuple(b.shape[1:])
+        plan, pad = getplan(vshape, b.dtype, "150")
         return [("swap", lambda: b.swap((0,), (0,)), ("perm", swap_perm(nd, b.split, (0,), (0,))[0])),
+                ("chunk", lambda: b.chunk("150"), ("packed", vshape, tuple(plan), tuple(pad))),
+                ("unchunk", lambda: b.chunk("150").unchunk(), ("perm", ident)),
                 ("var", lambda: b.var(axis=0), ("stat", "var", (0,), None))]
     if cfg == "C5":
+        v = tuple(b.shape[3:])
         return [("T", lambda: b.T, ("perm", rev)),
-                ("transpose", lambda: b.transpose(2, 0, 4, 1, 3), ("perm", [2, 0, 4, 1, 3]))]
+                ("transpose", lambda: b.transpose(2, 0, 4, 1, 3), ("perm", [2, 0, 4, 1, 3])),
+                ("chunk", lambda: b.chunk((16, 16), padding=2), ("packed", v, (16, 16), (2, 2))),
+                ("unchunk", lambda: b.chunk((16, 16), padding=2).unchunk(), ("perm", ident)),
+                # keys (k0, k1), values (k2, v0, v1): the moved key is one whole chunk
+                ("keys_to_values", lambda: b.chunk((16, 16), padding=2).keys_to_values((2,)),
+                 ("packed", (b.shape[2],) + v, (b.shape[2], 16, 16), (0, 2, 2))),
+                # keys (k0, k1, k2, v0), values (v1,)
+                ("values_to_keys", lambda: b.chunk((16, 16), padding=2).values_to_keys((0,)),
+                 ("packed", v[1:], (16,), (2,)))]
     if cfg == "target64":
         return [("swap", lambda: b.swap((0,), (0,)), ("perm", swap_perm(nd, b.split, (0,), (0,))[0])),
                 ("mean", lambda: b.mean(axis=0), ("stat", "mean", (0,), None)),
@@ -325,21 +367,21 @@ def _empty_cache(torch, dev):
 CHECK_CHUNK = 4 << 30  # bytes of the rebuilt array compared / reduced at a time
 
 
-def perm_check(torch, res, perm, shape, dtype, ctx, dev):
+def perm_check(torch, res, perm, gshape, dtype, ctx, dev):
     """True if this rank's slab of ``res`` equals x.transpose(perm), x the
-    global array whose rank-r rows are synth_shard(seed 1234 + r)."""
+    global array ``gshape`` whose rank-r slab is synth_shard(seed 1234 + r)."""
     world, es = ctx.world_size, np.dtype(dtype).itemsize
     idt = _int_type(torch, es)
-    gshape = (shape[0] * world,) + tuple(shape[1:])
+    slabs = slab_shapes(gshape, world)
     oshape = [gshape[p] for p in perm]
     got = res._data.view(idt)
     a, j = perm[0], perm.index(0)
     if world == 1 or a == 0:
         # this rank's own rows, permuted: compared in chunks of output rows
-        x = synth_shard(torch, shape, dtype, dev, 1234 + ctx.rank).view(idt).permute(*perm)
+        x = synth_shard(torch, slabs[ctx.rank], dtype, dev, 1234 + ctx.rank).view(idt).permute(*perm)
         row = int(np.prod(x.shape[1:]))
         step = max(1, CHECK_CHUNK // max(1, row * es))
-        ok = True
+        ok = got.numel() == x.numel()
         for lo in range(0, x.shape[0], step):
             hi = min(x.shape[0], lo + step)
             ok = ok and bool(torch.equal(got[lo * row:hi * row], x[lo:hi].contiguous().reshape(-1)))
@@ -348,12 +390,55 @@ def perm_check(torch, res, perm, shape, dtype, ctx, dev):
     lo, hi = ctx.bounds(oshape[0])[ctx.rank]
     want = torch.empty([hi - lo] + oshape[1:], dtype=idt, device=dev)
     for r, (rlo, rhi) in enumerate(ctx.bounds(gshape[0])):
-        x = synth_shard(torch, shape, dtype, dev, 1234 + r).view(idt)
+        x = synth_shard(torch, slabs[r], dtype, dev, 1234 + r).view(idt)
         want.narrow(j, rlo, rhi - rlo).copy_(x.narrow(a, lo, hi - lo).permute(*perm))
         del x
-    ok = bool(torch.equal(got, want.reshape(-1)))
+    ok = got.numel() == want.numel() and bool(torch.equal(got, want.reshape(-1)))
     del want
     return ok
+
+
+def _axis_slices(d, s, p):
+    """getslices (chunk.py:574-618) on one axis: chunk j = [j s - (j>0) p, j s + s + p) clipped."""
+    out, j = [], 0
+    while j * s < d:
+        out.append(slice(max(0, j * s - (p if j else 0)), min(d, j * s + s + p)))
+        j += 1
+    return out
+
+
+def packed_ref(torch, rec, vshape, plan, pad):
+    """(records, *vshape) tensor -> its packed chunk layout by torch slicing:
+    each record's chunks back to back in chunk-id (product) order, each a
+    dense box (test_gpu_large.py's rule, independent of plan.ChunkGeometry)."""
+    from itertools import product
+    sl = [_axis_slices(vshape[k], plan[k], pad[k]) for k in range(len(vshape))]
+    parts = [rec[(slice(None),) + tuple(c)].reshape(rec.shape[0], -1) for c in product(*sl)]
+    return torch.cat(parts, dim=1).reshape(-1)
+
+
+def packed_check(torch, res, vshape, plan, pad, gshape, dtype, ctx, dev):
+    """True if the chunked array ``res`` has plan / padding (plan, pad) and
+    this rank's packed bytes equal the slice rule on its records of x (records
+    never cross GPUs), compared in batches of records."""
+    if tuple(res.plan) != tuple(plan) or tuple(res.padding) != tuple(pad):
+        return False
+    es = np.dtype(dtype).itemsize
+    idt = _int_type(torch, es)
+    slab = slab_shapes(gshape, ctx.world_size)[ctx.rank]
+    x = synth_shard(torch, slab, dtype, dev, 1234 + ctx.rank).view(idt).reshape((-1,) + tuple(vshape))
+    got = res._packed.view(idt)
+    rec = int(np.prod(vshape))
+    batch = max(1, CHECK_CHUNK // max(1, 2 * rec * es))
+    ok, off = True, 0
+    for lo in range(0, x.shape[0], batch):
+        want = packed_ref(torch, x[lo:lo + batch], vshape, plan, pad)
+        n = want.numel()
+        ok = ok and off + n <= got.numel() and bool(torch.equal(got[off:off + n], want))
+        off += n
+        del want
+    del x
+    return ok and off == got.numel()
 
 
 def _as_f64(torch, t, dtype):
@@ -362,17 +447,17 @@ def _as_f64(torch, t, dtype):
     return t.to(torch.float64)
 
 
-def stat_truth(torch, name, axis, pre, shape, dtype, world, dev):
+def stat_truth(torch, name, axis, pre, gshape, dtype, world, dev):
     """(float64 truth, scale) of statistic ``name`` over ``axis`` of
     x.transpose(pre) on the device, x the global array rebuilt from every
     rank's seed.  Small arrays are rebuilt whole; otherwise (pre None, axis
     (0,)) each rank's rows are regenerated and reduced in chunks, merged with
     Chan's update.  ``scale`` is the tolerance's absolute term: max|x| (mean),
     sum|x| (sum), max|truth| (var / std)."""
-    es = np.dtype(dtype).itemsize
-    total = int(np.prod(shape)) * world * 8
+    slabs = slab_shapes(gshape, world)
+    total = int(np.prod(gshape)) * 8
     if total <= (1 << 30):
-        x = torch.cat([_as_f64(torch, synth_shard(torch, shape, dtype, dev, 1234 + r), dtype)
+        x = torch.cat([_as_f64(torch, synth_shard(torch, slabs[r], dtype, dev, 1234 + r), dtype)
                        for r in range(world)], 0)
         if pre is not None:
             x = x.permute(*pre)
@@ -386,12 +471,12 @@ def stat_truth(torch, name, axis, pre, shape, dtype, world, dev):
         return t, t.abs().max()
     if pre is not None or tuple(axis or ()) != (0,) or name not in ("mean", "var", "std"):
         raise ValueError("stat_truth: a large array is reduced over its leading axis only")
-    row = int(np.prod(shape[1:]))
+    row = int(np.prod(gshape[1:]))
     step = max(1, CHECK_CHUNK // (row * 8))
     n, mean, m2, xmax = 0, None, None, 0.0
     for r in range(world):
-        x = synth_shard(torch, shape, dtype, dev, 1234 + r)
-        for lo in range(0, shape[0], step):
+        x = synth_shard(torch, slabs[r], dtype, dev, 1234 + r)
+        for lo in range(0, slabs[r][0], step):
             c = _as_f64(torch, x[lo:lo + step], dtype)
             k = c.shape[0]
             cm = c.mean(0)
@@ -407,7 +492,6 @@ def stat_truth(torch, name, axis, pre, shape, dtype, world, dev):
                 n = tot
             del c, cq
         del x
-    del es
     if name == "mean":
         return mean, xmax
     v = m2 / n
@@ -436,23 +520,26 @@ def stat_within(got, truth, scale, name):
     return bool(np.all(err <= bar)), float(np.max(err / np.maximum(bar, 1e-300))) if err.size else 0.0
 
 
-def run_checks(torch, cfg, b, ctx, dev, shape, dtype, world):
-    """Every check of checks_of(cfg) on this rank -> {name: result}, all ranks'
-    verdicts merged (a mismatch on any rank is a mismatch)."""
+def run_checks(torch, cfg, b, ctx, dev, gshape, dtype, world):
+    """Every check of checks_of(cfg) on this rank -> ({name: verdict}, all ok);
+    all ranks' verdicts merged (a mismatch on any rank is a mismatch).
+    Verdicts: "exact" / "MISMATCH" (data movement), "ok <e>" / "FAIL <e>"
+    (statistics; e = largest error as a fraction of the tolerance bar)."""
     res = {}
     for name, call, spec in checks_of(cfg, b):
         r = call()
         if spec[0] == "perm":
-            ok = perm_check(torch, r, spec[1], shape, dtype, ctx, dev)
-            detail = "bit-exact" if ok else "MISMATCH"
+            ok = perm_check(torch, r, spec[1], gshape, dtype, ctx, dev)
+            detail = "exact" if ok else "MISMATCH"
+        elif spec[0] == "packed":
+            ok = packed_check(torch, r, spec[1], spec[2], spec[3], gshape, dtype, ctx, dev)
+            detail = "exact" if ok else "MISMATCH"
         else:
             _, stat, axis, pre = spec
-            truth, scale = stat_truth(torch, stat, axis, pre, shape, dtype, world, dev)
+            truth, scale = stat_truth(torch, stat, axis, pre, gshape, dtype, world, dev)
             ok, worst = stat_within(r, truth.cpu().numpy(), scale.cpu().numpy() if hasattr(scale, "cpu") else scale,
                                     stat)
-            detail = ("within %s (max error %.3g of the bar)" % (
-                "rtol 1e-12" if np.asarray(r).dtype == np.float64 else "rtol 1e-6", worst) if ok else
-                "OUT OF TOLERANCE (max error %.3g of the bar)" % worst)
+            detail = "%s %.3g" % ("ok" if ok else "FAIL", worst)
         del r
         _empty_cache(torch, dev)
         res[name] = (ok, detail)
@@ -466,15 +553,13 @@ def run_checks(torch, cfg, b, ctx, dev, shape, dtype, world):
     return {name: detail for name, (ok, detail) in res.items()}, all(ok for ok, _ in res.values())
 
 
-def exchange_check(torch, cfg, b, ctx, dev, shape=None, dtype=None, split=None):
+def exchange_check(torch, cfg, b, ctx, dev, gshape, dtype):
     """Bit-exact check of the first op of the step (the swap / .T that crosses
     GPUs): True if every byte of this rank's slab agrees with the global array
     rebuilt from every rank's seed."""
-    if shape is None:
-        shape, dtype, split, _ = CONFIGS[cfg]
     name, call, spec = checks_of(cfg, b)[0]
     r = call()
-    ok = perm_check(torch, r, spec[1], shape, dtype, ctx, dev)
+    ok = perm_check(torch, r, spec[1], gshape, dtype, ctx, dev)
     del r
     return ok
 
@@ -531,8 +616,8 @@ def pmc_traffic(cfg, args, nops, warmup=1, steps=2):
         cmd = [rp, "--pmc", ctr, "-d", out, "-o", "pmc", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--config", cfg, "--steps", str(steps),
                "--warmup", str(warmup), "--pmc-child"]
-        if args.shard_shapes:
-            cmd += ["--shard-shapes", args.shard_shapes]
+        if args.shapes:
+            cmd += ["--shapes", args.shapes]
         try:
             rc, _ = run_child(cmd, timeout=600)
         except OSError as e:  # profiler unavailable: report null
@@ -559,6 +644,217 @@ def pmc_traffic(cfg, args, nops, warmup=1, steps=2):
         per[ctr] = [float(np.median(vals[k::nops])) for k in range(nops)]
     traffic = [2.0 * f + w for f, w in zip(per["FETCH_SIZE"], per["WRITE_SIZE"])]
     return traffic, "per call: 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE over the library's kernels"
+
+
+# ------------------------------------------------ rocprofv3 at N > 1 ranks --
+
+PROFILED_ENV = "BOLT_AMD_BENCH_PROFILED"  # set in rank 0's profiled child: its trace directory
+
+
+def rocprof_path():
+    import shutil
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    return rp if os.path.exists(rp) else None
+
+
+def rocprof_wanted(args, world, where):
+    """True on EVERY rank of an N-rank GPU run whose rank 0 runs under
+    rocprofv3 (all ranks then run the marked pass, which holds collectives)."""
+    return (world > 1 and not args.no_rocprof and not args.pmc_child and where != "cpu"
+            and os.environ.get("BOLT_AMD_BENCH_ROCPROF", "1") != "0" and rocprof_path() is not None)
+
+
+def _die_with_parent():
+    """preexec: the child gets SIGKILL when the wrapper dies (PR_SET_PDEATHSIG)."""
+    import ctypes
+    import signal
+    try:
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGKILL), 0, 0, 0)
+    except OSError:
+        pass
+
+
+def rocprof_rank0(argv, world):
+    """Rank 0 of an N-rank run, before anything touches the GPU: run this
+    script again as rank 0 (same environment: it joins the rendezvous) under
+    ``rocprofv3 --kernel-trace --stats`` -- a fresh child, the program after
+    ``--`` -- then add the trace's numbers (rocprof_windows) to its JSON line
+    and relay it.  Exit status: the child's."""
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    out = tempfile.mkdtemp(prefix="bm_rocprof_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ)
+    env[PROFILED_ENV] = out
+    cmd = [rocprof_path(), "--kernel-trace", "--stats", "-d", out, "-o", "rank0", "--output-format", "csv",
+           "--", sys.executable, os.path.abspath(__file__)] + list(argv)
+    progress("rank 0 under rocprofv3 --kernel-trace --stats (%s)" % out)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, preexec_fn=_die_with_parent)
+    prev = signal.signal(signal.SIGTERM, lambda *_: p.terminate())
+    try:
+        raw, _ = p.communicate()
+    finally:
+        signal.signal(signal.SIGTERM, prev)
+    text = raw.decode("utf-8", "replace")
+    lines = [ln for ln in text.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        sys.stdout.write(text)
+        sys.stdout.flush()
+        shutil.rmtree(out, ignore_errors=True)
+        return p.returncode or 1
+    line = json.loads(lines[-1])
+    marks = line.pop("rocprof_marks", None)
+    info = line.pop("rocprof_info", {})
+    try:
+        traces = sorted(glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True))
+        if not traces:
+            raise RuntimeError("no kernel trace written")
+        kept = None
+        stats = sorted(glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True))
+        if stats:
+            keep_dir = os.path.join(HERE, "gpurun_out")
+            os.makedirs(keep_dir, exist_ok=True)
+            kept = os.path.join(keep_dir, "bench_rocprof_n%d_kernel_stats.csv" % world)
+            shutil.copyfile(stats[0], kept)
+            kept = os.path.relpath(kept, HERE)
+        merge_rocprof(line, rocprof_windows(traces[0], marks, info, world), kept)
+    except Exception as e:  # the measurement stands; the profile is reported missing
+        line["rocprof"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    shutil.rmtree(out, ignore_errors=True)
+    if line.get("detail"):
+        try:
+            path = os.path.join(HERE, line["detail"])
+            d = json.load(open(path))
+            d["rocprof"] = line.get("rocprof")
+            json.dump(d, open(path, "w"), indent=1)
+        except (OSError, ValueError):
+            pass
+    sys.stdout.write(json.dumps(line, separators=(",", ":")) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+def _short_kernel(name):
+    n = name.replace("(anonymous namespace)::", "")
+    return n[5:] if n.startswith("void ") else n
+
+
+def kernel_class(name):
+    """'marker' (torch's spin kernel), 'rccl', 'lib' (libbolt_mi355x), 'blit'
+    (the HIP runtime's copy kernels: hipMemcpyAsync on a shader) or 'other'."""
+    import re
+    n = _short_kernel(name)
+    if "spin_kernel" in n:
+        return "marker"
+    if re.search(r"nccl|rccl", n, re.I):
+        return "rccl"
+    if re.match(r"k_[a-z]", n):
+        return "lib"
+    if "rocclr" in n or "__amd" in n:
+        return "blit"
+    return "other"
+
+
+def _union_ms(iv):
+    """Length of the union of [start, end) intervals (ns) in ms."""
+    tot, cur = 0, None
+    for a, b in sorted(iv):
+        if cur is None or a > cur[1]:
+            if cur is not None:
+                tot += cur[1] - cur[0]
+            cur = [a, b]
+        else:
+            cur[1] = max(cur[1], b)
+    if cur is not None:
+        tot += cur[1] - cur[0]
+    return tot / 1e6
+
+
+def rocprof_windows(trace_csv, marks, info, world):
+    """Per op of the marked pass, from rank 0's kernel trace: the kernels that
+    ran between the op call's two marker kernels (on the current stream; the
+    exchange's RCCL kernels on the RCCL stream start after the call's first
+    marker and end before its last unpack, so before the second marker).
+
+    ``marks``: [[cfg, [op, ...], steps], ...] in the order the marked pass ran;
+    ``info``: {"cfg.op": [peer payload bytes per rank, pack+unpack bytes]}.
+    Returns {"cfg.op": {"n": calls, "span": ms between the markers, "rccl":
+    union of the RCCL kernels' intervals (ms per call), "rccl_n": RCCL kernels
+    per call, "lib": summed library kernel ms per call, "blit": runtime copy
+    kernels, and for an exchanging op "xgmi_GBs"/"xgmi_frac" (payload over the
+    RCCL time, of (G-1) x 153 GB/s) and "pu_frac" (pack + unpack bytes over the
+    library kernels' time, of 8 TB/s)}}."""
+    import csv
+    rows = []
+    for r in csv.DictReader(open(trace_csv)):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kernel_class(r["Kernel_Name"])))
+    rows.sort()
+    markers = [(a, b) for a, b, c in rows if c == "marker"]
+    calls = [("%s.%s" % (cfg, op)) for cfg, ops, steps in (marks or []) for _ in range(int(steps)) for op in ops]
+    if len(markers) != 2 * len(calls):
+        raise RuntimeError("%d marker kernels in the trace, %d expected" % (len(markers), 2 * len(calls)))
+    others = [(a, b, c) for a, b, c in rows if c != "marker"]
+    acc = {}
+    lo = 0
+    for k, label in enumerate(calls):
+        w0, w1 = markers[2 * k][1], markers[2 * k + 1][0]
+        while lo < len(others) and others[lo][0] < w0:
+            lo += 1
+        ks = []
+        i = lo
+        while i < len(others) and others[i][0] < w1:
+            ks.append(others[i])
+            i += 1
+        a = acc.setdefault(label, {"n": 0, "span": 0.0, "rccl": 0.0, "rccl_n": 0, "lib": 0.0, "blit": 0.0})
+        a["n"] += 1
+        a["span"] += (w1 - w0) / 1e6
+        a["rccl"] += _union_ms([(s, e) for s, e, c in ks if c == "rccl"])
+        a["rccl_n"] += sum(1 for _, _, c in ks if c == "rccl")
+        a["lib"] += sum(e - s for s, e, c in ks if c == "lib") / 1e6
+        a["blit"] += sum(e - s for s, e, c in ks if c == "blit") / 1e6
+    out = {}
+    peak = (world - 1) * XGMI_LINK_GBPS
+    for label, a in acc.items():
+        n = a["n"]
+        o = {"n": n, "span": round(a["span"] / n, 4), "rccl": round(a["rccl"] / n, 4),
+             "rccl_n": round(a["rccl_n"] / float(n), 2), "lib": round(a["lib"] / n, 4),
+             "blit": round(a["blit"] / n, 4)}
+        payload, local = (info or {}).get(label, (0, 0))
+        if payload and o["rccl"] > 0:
+            o["xgmi_GBs"] = round(payload / (o["rccl"] / 1e3) / 1e9, 1)
+            o["xgmi_frac"] = round(o["xgmi_GBs"] / peak, 4)
+        if payload and local and o["lib"] > 0:
+            o["pu_frac"] = round(local / (o["lib"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+        out[label] = o
+    return out
+
+
+def merge_rocprof(line, ops, stats_file):
+    """rocprof_windows' numbers into the record: ``rocprof`` (every op), the
+    headline swap's RCCL time into ``xgmi`` and each config op's into its
+    record."""
+    line["rocprof"] = {"rank": 0, "stats": stats_file, "ops": ops}
+    head = "%s.%s" % (line.get("config", {}).get("name", "C2"), next(iter(line.get("ops", {"swap": 0}))))
+    h = ops.get(head)
+    if h and "xgmi" in line:
+        line["xgmi"]["rocprof_ms"] = h["rccl"]
+        if "xgmi_GBs" in h:
+            line["xgmi"]["rocprof_achieved"] = h["xgmi_GBs"]
+            line["xgmi"]["rocprof_frac"] = h["xgmi_frac"]
+        if "pu_frac" in h:
+            line["xgmi"]["pack_unpack_frac"] = h["pu_frac"]
+    for cfg, rec in line.get("configs", {}).items():
+        for op, o in rec.get("ops", {}).items():
+            r = ops.get("%s.%s" % (cfg, op))
+            if r:
+                o["k_ms"] = r["lib"]
+                if r["rccl"]:
+                    o["rccl_ms"] = r["rccl"]
+                for k in ("xgmi_frac", "pu_frac"):
+                    if k in r:
+                        o[k] = r[k]
 
 
 # ------------------------------------------------------------ CPU baseline --
@@ -617,6 +913,8 @@ def local_numpy_baseline(cfg, shape, dtype):
         return parts, total
     el, (parts, total) = best_of(step)
     return {"value": total / el / 1e9, "unit": "GB/s", "cores": 1, "kind": "port", "reps": REPS,
+            "brief": "numpy local mode, %s %s slab, 1 core, best of 3" % (np.dtype(dtype).name,
+                                                                        str(sample_shape).replace(" ", "")),
             "sample": "the reference local mode's numpy calls on %s %s (a leading-axis slab of the "
                       "shard; chunk/unchunk not included), best of %d after 1 warm-up: %s"
                       % (np.dtype(dtype).name, str(sample_shape), REPS, " + ".join(parts)),
@@ -659,11 +957,13 @@ def c1_cpu_baseline(shape, dtype):
         el, _ = best_of(lambda: [f() for _ in range(reps)])
         out[name] = (total * reps / el / 1e9, reps)
     return {"value": out["spark"][0], "unit": "GB/s", "cores": 1, "kind": "port", "reps": REPS,
+            "brief": "oracle Spark-path port, whole C1, 1 core, best of 3",
             "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on the whole C1 input, "
                       "swap + sum/mean/var/std at axis=None and axis=(0,), %d steps per timed run, best of %d "
                       "after 1 warm-up" % (out["spark"][1], REPS),
             "host_cpus": os.cpu_count(),
             "local_numpy": {"value": round(out["local"][0], 3), "unit": "GB/s", "cores": 1, "reps": REPS,
+                            "brief": "numpy local mode, whole C1, 1 core",
                             "sample": "the reference local mode's numpy calls on the same input, %d steps per "
                                       "timed run, best of %d after 1 warm-up" % (out["local"][1], REPS)}}
 
@@ -671,7 +971,8 @@ def c1_cpu_baseline(shape, dtype):
 def cpu_baseline(cfg, shape, dtype, rows):
     """Oracle (record-level restatement of the reference Spark path), 1 core,
     bounded sample, best of 3 after 1 warm-up; C2 adds the local
-    mode's numpy calls, the Spark local[8] analogue and an OpenMP line."""
+    mode's numpy calls and an OpenMP line on the WHOLE C2 input, and the Spark
+    local[8] analogue on the oracle's sample."""
     from oracle import bolt_oracle as O
     if cfg == "C1":
         return c1_cpu_baseline(shape, dtype)
@@ -679,8 +980,9 @@ def cpu_baseline(cfg, shape, dtype, rows):
         return local_numpy_baseline(cfg, shape, dtype)
     rows = rows or C2_SAMPLE_ROWS
     rng = np.random.default_rng(0)
-    sample_shape = (rows,) + tuple(shape[1:])
-    x = (1000 + 50 * rng.standard_normal(sample_shape)).astype(dtype)
+    full = (1000 + 50 * rng.standard_normal(tuple(shape), dtype=np.float32)).astype(dtype, copy=False)
+    x = np.ascontiguousarray(full[:rows])
+    sample_shape = x.shape
     rs = O.parallelize(x, axis=(0,), npartitions=8)
 
     def spark():
@@ -697,30 +999,35 @@ def cpu_baseline(cfg, shape, dtype, rows):
         # the reference's local mode (bolt/local/array.py) runs the same three
         # calls as numpy on one host thread: ascontiguousarray(transpose) + mean / std
         u0 = time.perf_counter()
-        xs = np.ascontiguousarray(x.transpose(1, 2, 0))
+        xs = np.ascontiguousarray(full.transpose(1, 2, 0))
         u1 = time.perf_counter()
         xs.mean(axis=2)
         u2 = time.perf_counter()
         xs.std(axis=2)
         u3 = time.perf_counter()
+        del xs
         return u1 - u0, u2 - u1, u3 - u2
-    N = int(np.prod(sample_shape)) * np.dtype(dtype).itemsize
-    out_b = sample_shape[1] * sample_shape[2] * 4
-    total = 2 * N + 2 * (N + out_b)
+
+    def step_bytes(a):
+        N = a.nbytes
+        return 2 * N + 2 * (N + a.shape[1] * a.shape[2] * 4)
     ts, tp = best_of(spark)
     ls, lp = best_of(local)
-    out = {"value": total / ts / 1e9, "unit": "GB/s", "cores": 1, "kind": "port", "reps": REPS,
-           "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s, best of %d "
-                     "after 1 warm-up: swap((0,),(0,1)) %.2fs + mean(axis=2) %.2fs + std(axis=2) %.2fs"
-                     % ((str(sample_shape), REPS) + tp),
+    out = {"value": step_bytes(x) / ts / 1e9, "unit": "GB/s", "cores": 1, "kind": "port", "reps": REPS,
+           "brief": "oracle Spark-path port, f32 %s, 1 core, best of 3" % str(sample_shape).replace(" ", ""),
+           "sample": "oracle/bolt_oracle.py record-level Spark path (8 partitions) on float32 %s (the first %d "
+                     "time points of C2), best of %d after 1 warm-up: swap((0,),(0,1)) %.2fs + mean(axis=2) "
+                     "%.2fs + std(axis=2) %.2fs" % ((str(sample_shape), rows, REPS) + tp),
            "host_cpus": os.cpu_count(),
-           "local_numpy": {"value": round(total / ls / 1e9, 3), "unit": "GB/s", "cores": 1, "reps": REPS,
-                           "sample": "the reference local mode's numpy calls on the same input, best of %d "
-                                     "after 1 warm-up: transpose %.2fs + mean %.2fs + std %.2fs" % ((REPS,) + lp)}}
+           "local_numpy": {"value": round(step_bytes(full) / ls / 1e9, 3), "unit": "GB/s", "cores": 1,
+                           "reps": REPS, "brief": "numpy local mode, whole C2 f32 %s, 1 core, best of 3"
+                                                  % str(full.shape).replace(" ", ""),
+                           "sample": "the reference local mode's numpy calls on the whole C2 input float32 %s, "
+                                     "best of %d after 1 warm-up: transpose %.2fs + mean %.2fs + std %.2fs"
+                                     % ((str(full.shape), REPS) + lp)}}
     del rs
     out["spark_local8"] = spark_local8_baseline(x, dtype)
-    out["openmp"] = openmp_baseline(np.ascontiguousarray(
-        (1000 + 50 * rng.standard_normal((shape[0],) + tuple(shape[1:]), dtype=np.float32))))
+    out["openmp"] = openmp_baseline(full)
     return out
 
 
@@ -782,6 +1089,7 @@ def openmp_baseline(x):
     N = xc.nbytes
     total = 2 * N + 2 * (N + P * 4)
     out = {"value": round(total / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port", "reps": REPS,
+           "brief": "OpenMP local step, %d threads, f32 %s" % (threads, str(x.shape).replace(" ", "")),
            "sample": "oracle/c/local_step.c (OpenMP, the local mode's ascontiguousarray(transpose) + mean + "
                      "std) on float32 %s, best of %d after 1 warm-up: swap %.3fs + mean %.3fs + std %.3fs"
                      % ((str(x.shape), REPS) + parts)}
@@ -806,6 +1114,8 @@ def spark_local8_baseline(x, dtype, workers=8):
     out = x.shape[1] * x.shape[2] * 4
     total = 2 * N + 2 * (N + out)
     return {"value": round(total / t["total"] / 1e9, 4), "unit": "GB/s", "cores": workers, "reps": REPS,
+            "brief": "Spark local[%d] analogue, %d processes, f32 %s" % (workers, workers,
+                                                                        str(x.shape).replace(" ", "")),
             "kind": "port, local[%d] analogue" % workers, "host_cpus": os.cpu_count(),
             "sample": "oracle/spark_local.py on float32 %s, best of %d after 1 warm-up: stage 1 (%d map tasks: "
                       "chunk + relabel) %.2fs, stage 2 (%d reduce tasks: rebuild + values_to_keys + unchunk) "
@@ -821,8 +1131,8 @@ def cpu_baseline_in_child(args, cfg):
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", cfg]
     if args.cpu_sample_rows:
         cmd += ["--cpu-sample-rows", str(args.cpu_sample_rows)]
-    if args.shard_shapes:
-        cmd += ["--shard-shapes", args.shard_shapes]
+    if args.shapes:
+        cmd += ["--shapes", args.shapes]
     rc, out = run_child(cmd, timeout=900, capture=True)
     try:
         if rc != 0:
@@ -911,14 +1221,44 @@ def progress(msg):
 
 
 DTYPE_NAMES = {"float32": "f32", "float64": "f64", "uint16": "u16"}
+LEGEND = "profiles/BENCH_FIELDS.md"   # what every field of the record means (the prose lives there)
+
+
+def op_rec(nb, ms, launches=None):
+    """Compact per-op record: B algorithmic bytes per rank and call, ms per
+    call, frac of the 8 TB/s HBM peak, nl launches per call."""
+    o = {"B": int(nb), "ms": round(ms, 4) if ms else None}
+    if ms and nb:
+        o["frac"] = round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+    if launches is not None:
+        o["nl"] = round(launches, 2)
+    return o
+
+
+def compact_cpu(cb):
+    """The CPU baseline's numbers for the stdout record (its prose goes to the detail file)."""
+    if not isinstance(cb, dict) or cb.get("value") is None:
+        return cb
+    out = {"value": round(cb["value"], 4), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+           "sample": cb.get("brief", "")}
+    for k in ("local_numpy", "spark_local8", "openmp"):
+        v = cb.get(k)
+        if isinstance(v, dict):
+            out[k] = {"value": v.get("value"), "cores": v.get("cores"), "sample": v.get("brief", "")}
+    return out
+
+
+def detail_path(args, world):
+    p = args.detail or os.path.join("gpurun_out", "bench_detail_n%d.json" % world)
+    return p if os.path.isabs(p) else os.path.join(HERE, p)
 
 
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
     if args.cpu_baseline_child:
-        shape, dtype, split, _ = config_of(args, args.config)
-        print(json.dumps(cpu_baseline(args.config, shape, dtype, args.cpu_sample_rows)), flush=True)
+        gshape, dtype, _, _, _ = config_of(args, args.config)
+        print(json.dumps(cpu_baseline(args.config, gshape, dtype, args.cpu_sample_rows)), flush=True)
         return 0
     if env_world is None and (args.gpus or 1) > 1:
         return launch_ranks(args.gpus, sys.argv[1:])
@@ -936,6 +1276,9 @@ def main():
     if world > 1 and not rehearsal_knobs() and world > visible_gpus():
         sys.stderr.write("bench.py: WORLD_SIZE=%d but %d GPU(s) visible\n" % (world, visible_gpus()))
         return 2
+    profiling = rocprof_wanted(args, world, where)
+    if profiling and rank == 0 and not os.environ.get(PROFILED_ENV):
+        return rocprof_rank0(sys.argv[1:], world)
     import torch
     import torch.distributed as dist
     if where == "cpu":
@@ -969,6 +1312,8 @@ def main():
     if world > 1:
         _stdout_to_stderr(dist.barrier)  # (a lazily connecting transport talks here)
     be = backend_for(dev)
+    marks, marks_info = [], {}
+    prose = {}   # the detail file's descriptions
 
     def sync():
         if dev.type == "cuda":
@@ -988,12 +1333,11 @@ def main():
         return float(t.item())
 
     def build(cfg):
-        shape, dtype, split, desc = config_of(args, cfg)
-        gshape = (shape[0] * world,) + tuple(shape[1:])
-        shard = synth_shard(torch, shape, dtype, dev, 1234 + rank)
+        gshape, dtype, split, scaling, desc = config_of(args, cfg, world)
+        shard = synth_shard(torch, slab_shapes(gshape, world)[rank], dtype, dev, 1234 + rank)
         b = bolt.ConstructMI355X.fromshards(shard, gshape, context=ctx, split=split, dtype=dtype)
         del shard
-        return b, shape, dtype, split, desc, gshape
+        return b, gshape, dtype, split, scaling, desc
 
     def release():
         import gc
@@ -1023,19 +1367,60 @@ def main():
         barrier()
         return max_over_ranks(time.perf_counter() - t0)
 
-    def checks(cfg, b, shape, dtype):
+    def per_op_ms(ops, steps):
+        """{op: (ms per call, launches per call)}: one GPU, the library launches'
+        own hipEvents; N GPUs, hipEvents around each call (its exchange
+        included).  K more steps, outside the timed region."""
+        if world == 1:
+            clock = KernelClock(be, dev, LAUNCHES, pool=steps * len(ops) * 4)
+            try:
+                timed_steps(ops, steps, clock=clock)
+            finally:
+                clock.close()
+            return {name: (clock.ms(name, steps), clock.launches(name, steps)) for name, _, _ in ops}
+        calls = {}
+        timed_steps(ops, steps, call_events=calls)
+        return {name: (float(np.mean([a.elapsed_time(z) for a, z in calls[name]])) if calls.get(name) else None,
+                       None) for name, _, _ in ops}
+
+    def marked_pass(cfg, b, ops, steps):
+        """N ranks under rocprof: K more steps with torch's spin kernel as a
+        marker before and after every op call (every rank runs it: the ops
+        hold collectives); rank 0's trace attributes kernels to calls."""
+        if not profiling:
+            return
+        specs = {n: sp for n, _, sp in checks_of(cfg, b)}
+        for name, _, nb in ops:
+            sp = specs.get(name)
+            payload = 0
+            if sp and sp[0] == "perm" and sp[1][0] != 0:
+                payload = int(nb / 2 * (world - 1) / world)   # the permuted slab's bytes sent to peers
+            marks_info["%s.%s" % (cfg, name)] = [payload, int(2 * nb) if payload else 0]
+        progress("%s: marked pass (%d steps) for the kernel trace" % (cfg, steps))
+        barrier()
+        for _ in range(steps):
+            for name, call, _ in ops:
+                torch.cuda._sleep(1)
+                r = call()
+                del r
+                torch.cuda._sleep(1)
+        barrier()
+        marks.append([cfg, [n for n, _, _ in ops], steps])
+
+    def run_all_checks(cfg, b, gshape, dtype, rec_ops):
+        """Checks of every op (run_checks) into rec_ops[name]["ck"]; returns all-ok (None: skipped)."""
         if args.no_checks:
             return None
         progress("%s: checks" % cfg)
-        det, ok = run_checks(torch, cfg, b, ctx, dev, shape, dtype, world)
-        det["all"] = ("every result matches (permutes bit-exact, sharded-axis statistics within tolerance) "
-                      "against the global array rebuilt from each rank's seed" if ok else "FAILED")
-        return det
+        det, ok = run_checks(torch, cfg, b, ctx, dev, gshape, dtype, world)
+        for name, v in det.items():
+            rec_ops.setdefault(name, {})["ck"] = v
+        return ok
 
     def measure_main(cfg, steps, warmup):
-        """The headline line: wall time of K steps, the permute kernel's own
-        hipEvents (one GPU) or the exchange's (N GPUs)."""
-        b, shape, dtype, split, desc, gshape = build(cfg)
+        """The headline record: wall time of K steps, the permute kernel's own
+        hipEvents (one GPU) or the exchange's (N GPUs), per-op times, checks."""
+        b, gshape, dtype, split, scaling, desc = build(cfg)
         ops = steps_of(cfg, b, world)
         if args.pmc_child:  # profiled child of pmc_traffic(): the step, a marker before every op
             for _ in range(warmup + steps):
@@ -1091,60 +1476,52 @@ def main():
             "warmup": warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": DTYPE_NAMES[np.dtype(dtype).name],
-            "data": "synthetic (generated in HBM: 1000+50*N(0,1) float32 / N(0,1) float64 / uniform uint16)",
-            "config": {"workload": desc, "global_shape": list(gshape), "split": split,
-                       "parallelism": "dp%d (records sharded on the leading key axis)" % world,
-                       "collectives": ("none (single GPU)" if world == 1 else
-                                       "RCCL via libbolt_mi355x (bm_alltoallv / bm_allgatherv)" if ctx.comm
-                                       else "%s, host-staged (one-device rehearsal, not a measurement)" % backend),
+            "data": "synthetic, generated in HBM",
+            "config": {"name": cfg, "workload": desc, "global_shape": list(gshape), "split": split,
+                       "parallelism": "dp%d" % world,
+                       "collectives": ("none" if world == 1 else "rccl" if ctx.comm
+                                       else "%s host-staged (rehearsal)" % backend),
                        "bytes_per_step": {k: int(v) for k, v in per.items()}},
+            "legend": LEGEND,
             "roofline": {
                 "bound": "hbm",
-                "kernel": "bm_permute for the %s" % ops[0][0] if world == 1 else
-                          "swap = pack + all_to_all + unpack (per rank)",
+                "kernel": ("bm_permute (%s)" % ops[0][0]) if world == 1 else "swap exchange per rank",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": None,
                 "avg_ms": round(kern_ms, 4),
-                "swap_call_ms": round(swap_ms, 4),
                 "bytes_per_launch": int(swap_bytes_rank),
             },
         }
         if os.environ.get("BOLT_AMD_BENCH_LAUNCHER"):
-            line["launcher"] = os.environ["BOLT_AMD_BENCH_LAUNCHER"] + " (rank processes started by bench.py)"
+            line["launcher"] = os.environ["BOLT_AMD_BENCH_LAUNCHER"]
         if world > 1:
             G = world
-            xport = "RCCL" if ctx.comm else "%s (host-staged rehearsal)" % backend
             n_rank = ops[0][2] / 2                        # bytes held per rank
             payload = n_rank * (G - 1) / G                # bytes each rank sends to its peers
             ex = phases.get("exchange")
             if ex:  # the swap across GPUs: pipelined pack -> RCCL all-to-all -> unpack
-                line["roofline"].update({"kernel": "swap exchange per rank (pack + %s all_to_all + unpack, "
-                                                   "pipelined)" % xport,
-                                         "achieved": round(2 * n_rank / (ex / 1e3) / 1e9, 1),
+                line["roofline"].update({"achieved": round(2 * n_rank / (ex / 1e3) / 1e9, 1),
                                          "avg_ms": round(ex, 4), "bytes_per_launch": int(2 * n_rank)})
                 line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBPS, 4)
             peak = (G - 1) * XGMI_LINK_GBPS
-            line["xgmi"] = {"op": ("RCCL send/recv group (bm_alltoallv)" if ctx.comm else
-                                   "%s all_to_all" % xport) + " inside the pipelined swap exchange "
-                                  "(achieved = peer payload / whole exchange time: a lower bound)",
-                            "payload_bytes_per_rank": int(payload),
-                            "avg_ms": round(ex, 4) if ex else None,
-                            "achieved": round(payload / (ex / 1e3) / 1e9, 1) if ex else None,
-                            "peak": peak, "unit": "GB/s per rank (egress)",
-                            "frac": round(payload / (ex / 1e3) / 1e9 / peak, 4) if ex else None,
-                            "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
+            x = {"payload_bytes_per_rank": int(payload), "avg_ms": round(ex, 4) if ex else None,
+                 "achieved": round(payload / (ex / 1e3) / 1e9, 1) if ex else None, "peak": peak,
+                 "unit": "GB/s per rank (egress)",
+                 "frac": round(payload / (ex / 1e3) / 1e9 / peak, 4) if ex else None,
+                 "phases_ms": {k: round(v, 4) for k, v in phases.items()}}
             if rccl_ms:
                 # isolated: hipEvents around each bm_alltoallv on the RCCL stream
                 # (stages overlap pack / unpack, so this is the links' own time)
-                line["xgmi"]["rccl_ms_per_swap"] = round(rccl_ms, 4)
-                line["xgmi"]["rccl_achieved"] = round(payload / (rccl_ms / 1e3) / 1e9, 1)
-                line["xgmi"]["rccl_frac"] = round(payload / (rccl_ms / 1e3) / 1e9 / peak, 4)
+                x["rccl_ms_per_swap"] = round(rccl_ms, 4)
+                x["rccl_achieved"] = round(payload / (rccl_ms / 1e3) / 1e9, 1)
+                x["rccl_frac"] = round(payload / (rccl_ms / 1e3) / 1e9 / peak, 4)
+            line["xgmi"] = x
             if ctx.comm:
                 import ctypes
                 from bolt_amd.mi355x import _lib
@@ -1153,11 +1530,10 @@ def main():
                 _lib.check(_lib.load().bm_comm_info(ctx.comm, ctypes.byref(r_), ctypes.byref(w_), lib_path, 512),
                            "bm_comm_info")
                 line["rccl_ranks"] = int(w_.value)
-                line["rccl_lib"] = lib_path.value.decode("utf-8", "replace")
+                prose.setdefault("rccl_lib", lib_path.value.decode("utf-8", "replace"))
             else:
                 line["rccl_ranks"] = None
         line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
-        line["roofline"]["measured_copy_peak"] = HBM_COPY_GBPS
         stat_ops = [name for name, _, _ in ops[1:] if name in ("mean", "std", "var")]
         if stat_ops and world == 1:
             # the reduction kernels' own hipEvents, in K more steps (kept out of the
@@ -1167,36 +1543,21 @@ def main():
                 timed_steps(ops, steps, clock=clock, op_filter=stat_ops)
             finally:
                 clock.close()
-            sr = {"kernel": "bm_reduce (k_red_rows / k_red_cols) per statistic", "bound": "hbm",
-                  "peak": HBM_PEAK_GBPS, "unit": "GB/s"}
+            sr = {}
+            nbs = dict((n, v) for n, _, v in ops)
             for name in stat_ops:
                 ms = clock.ms(name, steps)
-                nb = dict((n, v) for n, _, v in ops)[name]
-                sr[name] = {"avg_ms": round(ms, 4), "bytes_per_launch": int(nb),
-                            "launches_per_call": clock.launches(name, steps),
-                            "achieved": round(nb / (ms / 1e3) / 1e9, 1),
-                            "frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None}
+                sr[name] = op_rec(nbs[name], ms, clock.launches(name, steps))
             line["stats_roofline"] = sr
-        if world == 1 and not args.pmc_child:
-            # every op's own library launches, in K more steps (per-op detail of
-            # the step; outside the timed region for the same reason)
-            clock = KernelClock(be, dev, LAUNCHES, pool=steps * len(ops) * 4)
-            try:
-                timed_steps(ops, steps, clock=clock)
-            finally:
-                clock.close()
-            line["ops"] = {}
-            for name, _, nb in ops:
-                ms = clock.ms(name, steps)
-                o = {"bytes": int(nb), "ms": round(ms, 4) if ms else None,
-                     "launches_per_call": clock.launches(name, steps)}
-                if ms and nb:
-                    o["achieved"] = round(nb / (ms / 1e3) / 1e9, 1)
-                    o["frac"] = round(o["achieved"] / HBM_PEAK_GBPS, 4)
-                line["ops"][name] = o
-        line["checks"] = checks(cfg, b, shape, dtype)
+        if not args.pmc_child:
+            # every op's own time, in K more steps (outside the timed region)
+            times = per_op_ms(ops, steps)
+            line["ops"] = {name: op_rec(nb, *times[name]) for name, _, nb in ops}
+        marked_pass(cfg, b, ops, steps)
+        ok = run_all_checks(cfg, b, gshape, dtype, line.setdefault("ops", {}))
+        line["checks_ok"] = ok
         if world > 1:
-            line["exchange_check"] = (line["checks"] or {}).get(ops[0][0])
+            line["exchange_check"] = line["ops"].get(ops[0][0], {}).get("ck")
         del b, ops
         release()
         return line
@@ -1204,7 +1565,7 @@ def main():
     def measure_sub(cfg, steps, warmup):
         """A sub-record: K steps of a config; per op the library launches' own
         hipEvents (one GPU) or each call's (N GPUs: the exchange included)."""
-        b, shape, dtype, split, desc, gshape = build(cfg)
+        b, gshape, dtype, split, scaling, desc = build(cfg)
         ops = steps_of(cfg, b, world)
         progress("%s: %d warm-up + %d timed steps on %d rank(s)" % (cfg, warmup, steps, world))
         for _ in range(warmup):
@@ -1222,46 +1583,36 @@ def main():
             if clock is not None:
                 clock.close()
         per = {name: nb * world for name, _, nb in ops}
-        rec = {"workload": desc, "global_shape": list(gshape), "split": split,
-               "dtype": DTYPE_NAMES[np.dtype(dtype).name],
-               "value": round(sum(per.values()) * steps / elapsed / 1e9, 2), "unit": "GB/s",
-               "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-               "timing": ("hipEvents around each library launch on its stream, summed per op call" if world == 1
-                          else "hipEvents around each call on the current stream (the RCCL exchange included)"),
-               "ops": {}}
+        rec = {"value": round(sum(per.values()) * steps / elapsed / 1e9, 2),
+               "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "scaling": scaling,
+               "global_shape": list(gshape), "dtype": DTYPE_NAMES[np.dtype(dtype).name], "ops": {}}
+        prose.setdefault("workloads", {})[cfg] = desc
         for name, _, nb in ops:
             if clock is not None:
-                ms = clock.ms(name, steps)
-                nl = clock.launches(name, steps)
+                ms, nl = clock.ms(name, steps), clock.launches(name, steps)
             else:
                 evs = calls.get(name, [])
-                ms = float(np.mean([a.elapsed_time(z) for a, z in evs])) if evs else None
-                nl = None
-            o = {"bytes": int(nb), "ms": round(ms, 4) if ms else None, "launches_per_call": nl}
-            if ms and nb:
-                o["achieved"] = round(nb / (ms / 1e3) / 1e9, 1)
-                o["frac"] = round(o["achieved"] / HBM_PEAK_GBPS, 4)
-            rec["ops"][name] = o
+                ms, nl = (float(np.mean([a.elapsed_time(z) for a, z in evs])) if evs else None), None
+            rec["ops"][name] = op_rec(nb, ms, nl)
         timed = [(o["ms"], n) for n, o in rec["ops"].items() if o["ms"]]
         rec["dominant"] = max(timed)[1] if timed else None
-        rec["checks"] = checks(cfg, b, shape, dtype)
+        marked_pass(cfg, b, ops, steps)
+        rec["ok"] = run_all_checks(cfg, b, gshape, dtype, rec["ops"])
         del b, ops
         release()
         return rec
 
-    def add_traffic(cfg, names, into):
-        """PMC traffic per op call (rank 0, one GPU), into {name: record}."""
+    def add_traffic(cfg, names, recs):
+        """PMC traffic per op call (rank 0, one GPU): "tr" = traffic / algorithmic bytes."""
         progress("%s: rocprofv3 --pmc passes" % cfg)
         traffic, note = pmc_traffic(cfg, args, len(names))
+        prose.setdefault("traffic", note)
         for k, name in enumerate(names):
-            rec = into.get(name)
-            if rec is None:
-                continue
-            rec["traffic"] = int(traffic[k]) if traffic else None
-            nb = rec.get("bytes", rec.get("bytes_per_launch"))
-            if traffic and nb:
-                rec["traffic_ratio"] = round(traffic[k] / nb, 4)
-        return note
+            for rec in recs.get(name, ()):
+                nb = rec.get("B", rec.get("bytes_per_launch"))
+                if traffic and nb:
+                    rec["tr"] = round(traffic[k] / nb, 4)
+        return traffic
 
     line = measure_main(args.config, args.steps, args.warmup)
     if line is None:
@@ -1269,45 +1620,79 @@ def main():
     one = rank == 0 and world == 1 and dev.type == "cuda"
     if one and not args.no_pmc:
         names = list(line["config"]["bytes_per_step"])
-        recs = {names[0]: line["roofline"]}
-        recs.update({n: v for n, v in line.get("stats_roofline", {}).items() if isinstance(v, dict)})
-        # every other op of the step: its traffic against its algorithmic bytes
-        recs.update({n: o for n, o in line.get("ops", {}).items() if n not in recs})
-        line["roofline"]["traffic_note"] = add_traffic(args.config, names, recs)
-        for n, o in line.get("ops", {}).items():
-            src = recs.get(n)
-            if src is not o and src is not None and "traffic" in src:
-                o["traffic"] = src["traffic"]
-                if "traffic_ratio" in src:
-                    o["traffic_ratio"] = src["traffic_ratio"]
+        recs = {n: [line["ops"][n]] for n in names if n in line["ops"]}
+        recs.setdefault(names[0], []).append(line["roofline"])
+        for n, v in line.get("stats_roofline", {}).items():
+            recs.setdefault(n, []).append(v)
+        traffic = add_traffic(args.config, names, recs)
+        if traffic:
+            line["roofline"]["traffic"] = int(traffic[0])
+            line["roofline"]["traffic_ratio"] = line["roofline"].pop("tr", None)
+    target = None
     if world == 1 and args.config == "C2" and not args.no_target64:
         # BASELINE.json's target sentence: swap and statistics of a 64 GiB
         # float32 4-D array on one GPU at >= 60% of the HBM roofline
         t = measure_main("target64", args.target_steps, 1)
-        sub = {"workload": t["config"]["workload"], "value": t["value"], "unit": "GB/s",
-               "ms_per_step": t["ms_per_step"], "steps": t["steps"], "warmup": t["warmup"],
-               "global_shape": t["config"]["global_shape"], "bytes_per_step": t["config"]["bytes_per_step"],
-               "frac_of_hbm_peak": round(t["value"] / HBM_PEAK_GBPS, 4),
-               "target": "swap + mean/std of 64 GiB on 1 GPU at >= 0.60 of HBM (swap <= 28.6 ms)",
-               "roofline": t["roofline"], "stats_roofline": t.get("stats_roofline"), "checks": t["checks"]}
+        target = {"value": t["value"], "frac_of_hbm_peak": round(t["value"] / HBM_PEAK_GBPS, 4),
+                  "ms_per_step": t["ms_per_step"], "steps": t["steps"], "global_shape": t["config"]["global_shape"],
+                  "target": "value >= 0.60 x 8 TB/s on one GPU",
+                  "roofline": {k: t["roofline"][k] for k in ("achieved", "frac", "avg_ms", "bytes_per_launch")},
+                  "ops": t["ops"], "ok": t["checks_ok"]}
+        prose.setdefault("workloads", {})["target64"] = t["config"]["workload"]
         if one and not args.no_pmc:
             names = list(t["config"]["bytes_per_step"])
-            recs = {names[0]: sub["roofline"]}
-            recs.update({n: v for n, v in (sub["stats_roofline"] or {}).items() if isinstance(v, dict)})
-            sub["roofline"]["traffic_note"] = add_traffic("target64", names, recs)
-        line["target64"] = sub
+            recs = {n: [target["ops"][n]] for n in names if n in target["ops"]}
+            recs[names[0]].append(target["roofline"])
+            add_traffic("target64", names, recs)
+            target["roofline"]["traffic_ratio"] = target["roofline"].pop("tr", None)
+    configs = None
     if args.config == "C2" and not args.no_configs:
-        line["configs"] = {}
+        configs = {}
         for cfg in SUB_CONFIGS:
             rec = measure_sub(cfg, args.config_steps, 1)
             if one and not args.no_pmc:
-                rec["traffic_note"] = add_traffic(cfg, list(rec["ops"]), rec["ops"])
-            line["configs"][cfg] = rec
+                add_traffic(cfg, list(rec["ops"]), {n: [o] for n, o in rec["ops"].items()})
+            configs[cfg] = rec
+    cpu = None
     if one and not args.no_cpu_baseline:
         progress("%s: CPU baseline (child process)" % args.config)
-        line["cpu_baseline"] = cpu_baseline_in_child(args, args.config)
+        cpu = cpu_baseline_in_child(args, args.config)
+    # the stdout record: the driver keeps its tail, so the numbers come after
+    # the contract keys in this order and the prose goes to the detail file
+    out = dict(line)
+    stats_roofline = out.pop("stats_roofline", None)
+    ops = out.pop("ops", None)
+    checks_ok = out.pop("checks_ok", None)
+    if cpu is not None:
+        out["cpu_baseline"] = compact_cpu(cpu)
+    out["ops"] = ops
+    if configs is not None:
+        out["configs"] = configs
+    if target is not None:
+        out["target64"] = target
+    if stats_roofline is not None:
+        out["stats_roofline"] = stats_roofline
+    out["checks_ok"] = checks_ok
+    if profiling:
+        out["rocprof_marks"] = marks
+        out["rocprof_info"] = marks_info
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        path = detail_path(args, world)
+        try:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            d = dict(out)
+            d.pop("rocprof_marks", None)
+            d.pop("rocprof_info", None)
+            prose.setdefault("workloads", {})[args.config] = line["config"]["workload"]
+            d["prose"] = prose
+            if cpu is not None:
+                d["cpu_baseline"] = cpu
+            with open(path, "w") as f:
+                json.dump(d, f, indent=1)
+            out["detail"] = os.path.relpath(path, HERE)
+        except OSError as e:
+            out["detail"] = "not written: %s" % e
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     if world > 1:
         barrier()
         ctx.close()  # the library's RCCL communicator, before the process group

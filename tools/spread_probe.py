@@ -35,7 +35,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     ctx = bolt.MI355XContext(device=dev)
-    shape, dtype, split, _ = bench.CONFIGS[args.config]
+    shape, dtype, split, _, _ = bench.CONFIGS[args.config]
     shard = bench.synth_shard(torch, shape, dtype, dev, 1234)
     b = bolt.ConstructMI355X.fromshards(shard, shape, context=ctx, split=split, dtype=dtype)
     del shard
