@@ -35,19 +35,7 @@ constexpr int kCThreads = 256;
 constexpr int64_t kStageBytes = 32768;   // LDS per tile when records are small (5 blocks / CU)
 constexpr int64_t kMaxStageBytes = 65536;
 constexpr int kMaxParts = 8;
-#ifndef BM_RECMAP_XCDREG
-// 1: the tiles of the blocks dealt to XCD x (blockIdx % 8 under round-robin
-// dispatch) come from the x-th eighth of the records, so the eight XCDs stream
-// eight separate regions at once instead of one contiguous window (A/B knob;
-// applied when the tile count is a multiple of 8)
-#define BM_RECMAP_XCDREG 0
-#endif
-#ifndef BM_STAGE_MASK
-#define BM_STAGE_MASK 1  // 0: ignore stage masks, stage whole ranges (A/B knob)
-#endif
-#ifndef BM_RECMAP_GRIDCAP
-#define BM_RECMAP_GRIDCAP 16384  // blocks per launch, then grid-stride over tiles (A/B knob)
-#endif
+constexpr int kRecmapGridCap = 16384;  // blocks per launch, then grid-stride over tiles
 
 template <int ES> struct Elem;
 template <> struct Elem<1> { typedef uint8_t t; };
@@ -62,25 +50,12 @@ struct Parts {
 };
 
 // Stage n L-vectors of a contiguous source range into LDS, kStageU loads in
-// flight per lane (a one-load-then-wait loop left the kernel latency-bound).
-#ifndef BM_STAGE_U
-#define BM_STAGE_U 8
-#endif
-#ifndef BM_RECMAP_NT
-#define BM_RECMAP_NT 3  // bit 0: non-temporal staging loads, bit 1: non-temporal stores (A/B knob)
-#endif
-template <typename V> __device__ __forceinline__ V ld_src(const V *p) {
-  if (BM_RECMAP_NT & 1) return __builtin_nontemporal_load(p);
-  return *p;
-}
-template <typename V> __device__ __forceinline__ void st_dst(V v, V *p) {
-  if (BM_RECMAP_NT & 2) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-#ifndef BM_GATHER_U
-#define BM_GATHER_U 0  // 0: 16 B of map per lane per round
-#endif
-constexpr int kStageU = BM_STAGE_U;
+// flight per lane (a one-load-then-wait loop left the kernel latency-bound;
+// 4 or 16 in flight measured +-0.5%, profiles/r04i_pack_knobs.log).  Records
+// are read and written once: non-temporal loads and stores.
+template <typename V> __device__ __forceinline__ V ld_src(const V *p) { return __builtin_nontemporal_load(p); }
+template <typename V> __device__ __forceinline__ void st_dst(V v, V *p) { __builtin_nontemporal_store(v, p); }
+constexpr int kStageU = 8;
 template <typename L>
 __device__ __forceinline__ void stage_lds(L *sl, const L *s, int64_t n) {
   for (int64_t i0 = threadIdx.x; i0 < n; i0 += (int64_t)kStageU * kCThreads) {
@@ -121,10 +96,11 @@ __device__ __forceinline__ void stage_lds_masked(L *sl, const L *s, int64_t n, c
   }
 }
 
-// destination vectors per lane per gather round: their map reads go out together
+// destination vectors per lane per gather round (16 B of map per lane): their
+// map reads go out together
 template <int VEC>
 struct GatherU {
-  static constexpr int v = BM_GATHER_U > 0 ? BM_GATHER_U : (VEC >= 8 ? 2 : 16 / VEC);
+  static constexpr int v = VEC >= 8 ? 2 : 16 / VEC;
 };
 
 // LB: staging load width in bytes (16 when the tile's bytes are 16-B aligned)
@@ -138,9 +114,7 @@ __global__ void __launch_bounds__(kCThreads)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = (nrec + rb - 1) / rb;
-  const bool reg = BM_RECMAP_XCDREG && ntiles % 8 == 0 && gridDim.x % 8 == 0;
-  for (int64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-    const int64_t t = reg ? (t0 % 8) * (ntiles / 8) + t0 / 8 : t0;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t r0 = t * rb;
     const int64_t nr = min(rb, nrec - r0);
     // stage nr contiguous source records
@@ -195,14 +169,12 @@ __global__ void __launch_bounds__(kCThreads)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const T *lds = reinterpret_cast<const T *>(smem);
   const int64_t ntiles = nrec * P.n;
-  const bool reg = BM_RECMAP_XCDREG && ntiles % 8 == 0 && gridDim.x % 8 == 0;
   uint32_t *lmask = reinterpret_cast<uint32_t *>(smem + mask_off);
   if (mask) {  // every part's unit mask, once per block
     for (int i = threadIdx.x; i < P.n * mask_words; i += kCThreads) lmask[i] = mask[i];
     __syncthreads();
   }
-  for (int64_t t0 = blockIdx.x; t0 < ntiles; t0 += gridDim.x) {
-    const int64_t t = reg ? (t0 % 8) * (ntiles / 8) + t0 / 8 : t0;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t r = t / P.n;
     const int p = (int)(t - r * P.n);
     const int64_t slo = P.slo[p], dlo = P.dlo[p];
@@ -267,19 +239,17 @@ __global__ void __launch_bounds__(kCThreads)
 // the trailing keys (group = their extent, map_b = box sizes), values_to_keys
 // and unchunk (group 1).  Reads are one contiguous stream; writes are
 // contiguous runs of whole boxes, adjacent across consecutive records.
-#ifndef BM_SCATTER_U
-#define BM_SCATTER_U 1  // source vectors per lane per round, all in flight together (A/B knob)
-#endif
-#ifndef BM_SCATTER_SPEC
-#define BM_SCATTER_SPEC 0  // 1: load the source vector before its map entry arrives (A/B knob)
-#endif
+// One source vector per lane per round (U = 2..8 in flight measured
+// -4..-17%: a wave's vectors then sit 4 KiB apart; a speculative source load
+// before the map entry arrives -1.5%, profiles/r04b_scatter_u.log).
+constexpr int kScatterU = 1;
 template <int ES, int VEC>
 __global__ void __launch_bounds__(kCThreads)
     k_recmap_scatter(const char *__restrict__ src, char *__restrict__ dst, const int32_t *__restrict__ ma,
                      const int32_t *__restrict__ mb, uint64_t total, FastDiv fvpr, FastDiv fgroup,
                      int64_t gstride) {
   typedef typename VecB<ES * VEC>::t V;
-  constexpr int U = BM_SCATTER_U;
+  constexpr int U = kScatterU;
   const uint64_t step = (uint64_t)gridDim.x * kCThreads * U;
   for (uint64_t i0 = (uint64_t)blockIdx.x * kCThreads * U + threadIdx.x; i0 < total; i0 += step) {
     V x[U];
@@ -289,7 +259,6 @@ __global__ void __launch_bounds__(kCThreads)
       const uint64_t i = i0 + (uint64_t)u * kCThreads;
       d[u] = -1;
       if (i < total) {
-        if (BM_SCATTER_SPEC) x[u] = ld_src(reinterpret_cast<const V *>(src) + i);
         const uint64_t r = fd_div(i, fvpr);
         const int64_t p = (int64_t)(i - r * fvpr.d) * VEC;
         const int32_t a = ma[p];
@@ -297,7 +266,7 @@ __global__ void __launch_bounds__(kCThreads)
           const uint64_t hi = fd_div(r, fgroup);
           d[u] = (int64_t)hi * gstride + a;
           if (mb) d[u] += (int64_t)(r - hi * fgroup.d) * mb[p];
-          if (!BM_SCATTER_SPEC) x[u] = ld_src(reinterpret_cast<const V *>(src) + i);
+          x[u] = ld_src(reinterpret_cast<const V *>(src) + i);
         }
       }
     }
@@ -312,7 +281,7 @@ void launch_scatter(const char *src, char *dst, const int32_t *ma, const int32_t
                     int64_t src_rec, int64_t group, int64_t gstride, int vec, hipStream_t st) {
   const uint64_t vpr = (uint64_t)(src_rec / vec);
   const uint64_t total = (uint64_t)nrec * vpr;
-  uint64_t g = (total + (uint64_t)kCThreads * BM_SCATTER_U - 1) / ((uint64_t)kCThreads * BM_SCATTER_U);
+  uint64_t g = (total + (uint64_t)kCThreads * kScatterU - 1) / ((uint64_t)kCThreads * kScatterU);
   if (g > 16777215ull) g = 16777215ull;  // HIP launch limit, then grid-stride
   const FastDiv fv = make_fastdiv(vpr), fg = make_fastdiv((uint64_t)group);
   constexpr int V16 = 16 / ES;
@@ -335,41 +304,28 @@ void launch_scatter(const char *src, char *dst, const int32_t *ma, const int32_t
 // each contiguous in the source record and in its new record).  Run b of
 // record r (r = g * group + k):
 //     dst[g * gstride + a_b + k * m_b + j] = src[r * src_rec + s_b + j],  j < len_b
-// One wave per (record, run) unit, no maps: every lane's loads issue at once,
-// U vectors in flight per lane, and a wave writes one contiguous run.
-// DMAJOR: units ordered by destination (the group's runs b, then k), so the
-// waves in flight write consecutive runs of one new record; else by source.
+// One wave per (record, run) unit, ordered by source (u = r * nruns + b), no
+// maps: every lane's loads issue at once, kRunsU vectors in flight per lane,
+// and a wave writes one contiguous run.  (Destination-major unit order ran
+// within 0.6% of it, profiles/r04b_runs.log; runs that tile the new records
+// take the destination walk below instead.)
 // Runs table: DEVICE int64 [s, len, a, m] x nruns, in VB-byte vectors.
-#ifndef BM_RUNS_U
-#define BM_RUNS_U 4
-#endif
-#ifndef BM_RUNS_DMAJOR
-#define BM_RUNS_DMAJOR 0
-#endif
-template <int VB, int U, bool DMAJOR>
+constexpr int kRunsU = 4;
+template <int VB>
 __global__ void __launch_bounds__(kCThreads)
     k_record_runs(const char *__restrict__ src, char *__restrict__ dst, const int64_t *__restrict__ runs,
                   int nruns, uint64_t nunits, int64_t src_rec, int64_t gstride, FastDiv fruns, FastDiv fgroup) {
   typedef typename VecB<VB>::t V;
+  constexpr int U = kRunsU;
   const V *s = reinterpret_cast<const V *>(src);
   V *d = reinterpret_cast<V *>(dst);
   const int lane = threadIdx.x & 63;
   const uint64_t nw = (uint64_t)gridDim.x * (kCThreads / 64);
   for (uint64_t u = (uint64_t)blockIdx.x * (kCThreads / 64) + (threadIdx.x >> 6); u < nunits; u += nw) {
-    uint64_t r, g, k;
-    int b;
-    if (DMAJOR) {  // u = (g * nruns + b) * group + k
-      const uint64_t q = fd_div(u, fgroup);
-      k = u - q * fgroup.d;
-      g = fd_div(q, fruns);
-      b = (int)(q - g * fruns.d);
-      r = g * fgroup.d + k;
-    } else {  // u = r * nruns + b
-      r = fd_div(u, fruns);
-      b = (int)(u - r * fruns.d);
-      g = fd_div(r, fgroup);
-      k = r - g * fgroup.d;
-    }
+    const uint64_t r = fd_div(u, fruns);
+    const int b = (int)(u - r * fruns.d);
+    const uint64_t g = fd_div(r, fgroup);
+    const uint64_t k = r - g * fgroup.d;
     const int64_t *e = runs + 4 * b;
     const int64_t len = e[1];
     const V *sp = s + (int64_t)r * src_rec + e[0];
@@ -391,23 +347,12 @@ __global__ void __launch_bounds__(kCThreads)
 // in order -- every wave writes 64 * U consecutive vectors, whole lines -- and
 // each finds its source: run b by binary search over the runs (sorted by a,
 // staged in LDS), k = (o - a_b) / len_b, then the source record g * group + k.
-#ifndef BM_RUNS_DWALK
-#define BM_RUNS_DWALK 1
-#endif
-#ifndef BM_RUNS_DWALK_U
-#define BM_RUNS_DWALK_U 2
-#endif
-#ifndef BM_RUNS_XCD
-// 1: the blocks of one XCD walk one contiguous eighth of the destination.
-// With temporal source loads (BM_RUNS_TLOAD) a source line that two chunk
-// boxes of a record share is then read again a region later from the same
-// XCD's L2: PMC traffic 1.0375x -> 1.0000x and +0.7..+2.5% on C5's
-// keys_to_values (profiles/r04o_runs_xcd.log)
-#define BM_RUNS_XCD 1
-#endif
-#ifndef BM_RUNS_TLOAD
-#define BM_RUNS_TLOAD 1  // destination walk: temporal source loads (0: non-temporal, A/B knob)
-#endif
+// kWalkU = 2 vectors per lane beats 1 (-1.7%) and 4 (-2.5%); the blocks of
+// one XCD walk one contiguous eighth of the destination, and the source loads
+// are temporal: a source line two chunk boxes of a record share is then read
+// again a region later from the same XCD's L2 (PMC traffic 1.0375x ->
+// 1.0000x, +0.7..+2.5% on C5's keys_to_values, profiles/r04o_runs_xcd.log).
+constexpr int kWalkU = 2;
 constexpr int kMaxWalkRuns = 64;
 template <int VB, int U>
 __global__ void __launch_bounds__(kCThreads)
@@ -425,10 +370,10 @@ __global__ void __launch_bounds__(kCThreads)
   const uint64_t per_block = (uint64_t)kCThreads * U;
   const uint64_t wave0 = (uint64_t)(threadIdx.x >> 6) * 64 * U;
   const uint64_t nwork = (total + per_block - 1) / per_block;
-  // BM_RUNS_XCD: the blocks of one XCD (w % 8 under round-robin dispatch;
-  // the grid is a multiple of 8) take one contiguous eighth of the
-  // destination (affinity only: any block-to-XCD mapping is correct)
-  const bool xcd = BM_RUNS_XCD && nwork % 8 == 0 && gridDim.x % 8 == 0;
+  // the blocks of one XCD (w % 8 under round-robin dispatch; the grid is a
+  // multiple of 8) take one contiguous eighth of the destination (affinity
+  // only: any block-to-XCD mapping is correct)
+  const bool xcd = nwork % 8 == 0 && gridDim.x % 8 == 0;
   for (uint64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
     const uint64_t base = (xcd ? (w % 8) * (nwork / 8) + w / 8 : w) * per_block;
     V x[U];
@@ -449,7 +394,7 @@ __global__ void __launch_bounds__(kCThreads)
         if (k * len > off) --k;
         else if ((k + 1) * len <= off) ++k;
         const V *sp = s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + (off - k * len);
-        x[u] = BM_RUNS_TLOAD ? *sp : ld_src(sp);
+        x[u] = *sp;  // temporal: the shared line's second read hits L2
       }
     }
 #pragma unroll
@@ -463,21 +408,20 @@ __global__ void __launch_bounds__(kCThreads)
 template <int VB>
 void launch_runs(const char *src, char *dst, const int64_t *runs, int nruns, int64_t nrec, int64_t src_rec,
                  int64_t group, int64_t gstride, bool tiled, hipStream_t st) {
-  if (BM_RUNS_DWALK && tiled) {
+  if (tiled) {
     const uint64_t total = (uint64_t)(nrec / group) * (uint64_t)gstride;
-    const uint64_t per_block = (uint64_t)kCThreads * BM_RUNS_DWALK_U;
+    const uint64_t per_block = (uint64_t)kCThreads * kWalkU;
     uint64_t g = (total + per_block - 1) / per_block;
     if (g > 1048576) g = 1048576;
-    k_record_runs_dst<VB, BM_RUNS_DWALK_U><<<(int)g, kCThreads, 0, st>>>(src, dst, runs, nruns, total, src_rec,
-                                                                        group, make_fastdiv((uint64_t)gstride));
+    k_record_runs_dst<VB, kWalkU><<<(int)g, kCThreads, 0, st>>>(src, dst, runs, nruns, total, src_rec, group,
+                                                               make_fastdiv((uint64_t)gstride));
     return;
   }
   const uint64_t nunits = (uint64_t)nrec * (uint64_t)nruns;
   uint64_t g = (nunits + kCThreads / 64 - 1) / (kCThreads / 64);
   if (g > 1048576) g = 1048576;  // then grid-stride over units
   const FastDiv fr = make_fastdiv((uint64_t)nruns), fg = make_fastdiv((uint64_t)group);
-  k_record_runs<VB, BM_RUNS_U, BM_RUNS_DMAJOR != 0><<<(int)g, kCThreads, 0, st>>>(
-      src, dst, runs, nruns, nunits, src_rec, gstride, fr, fg);
+  k_record_runs<VB><<<(int)g, kCThreads, 0, st>>>(src, dst, runs, nruns, nunits, src_rec, gstride, fr, fg);
 }
 
 struct Launch {
@@ -606,7 +550,7 @@ extern "C" int bm_record_gather_masked(const void *src_, void *dst_, int64_t nre
       L.mask = nullptr;
       L.mask_words = 0;
       L.mask_off = (int64_t)L.shmem;
-      if (BM_STAGE_MASK && stage_mask && mask_words > 0) {
+      if (stage_mask && mask_words > 0) {
         // one bit per 16-B unit of the widest range (checked against it), all parts' masks in LDS
         if ((int64_t)mask_words * 32 * 16 < span * es) {
           bm_set_error("bm_record_gather: %d mask words cannot cover %lld-B ranges", mask_words,
@@ -629,7 +573,7 @@ extern "C" int bm_record_gather_masked(const void *src_, void *dst_, int64_t nre
       L.shmem = (size_t)(rb * rec_bytes + 15) / 16 * 16;
       ntiles = (nrec + rb - 1) / rb;
     }
-    L.grid = (int)(ntiles < BM_RECMAP_GRIDCAP ? ntiles : BM_RECMAP_GRIDCAP);
+    L.grid = (int)(ntiles < kRecmapGridCap ? ntiles : kRecmapGridCap);
     const int vec = std::max(1, vb / es);
     switch (es) {
       case 1: launch_lds<1>(L, lb, vec); break;

@@ -30,141 +30,41 @@
 namespace {
 
 constexpr int kThreads = 256;
-// rowcopy launch shape (A/B knobs, tools/ab_bench.py)
-#ifndef BM_RC_THREADS
-#define BM_RC_THREADS 256
-#endif
-#ifndef BM_RC_UNROLL
-#define BM_RC_UNROLL 1
-#endif
-#ifndef BM_RC_GRIDCAP
-#define BM_RC_GRIDCAP 16777208  // one vector per lane, a block per 256 vectors, up to the 2^32-thread launch limit
-                                // (profiles/r01_ab3..ab5: many blocks +15-25% on C3/C4 swaps)
-#endif
-#ifndef BM_PK
-#define BM_PK 1  // packed-word tiles for 1-/2-byte transposes (A/B knob)
-#endif
-#ifndef BM_PK16_TA  // packed tiles, profiles/r01_ab_pk2.log: u16 128x256 +9%, u8 128x256 +11% over
-#define BM_PK16_TA 128  // element-wise LDS tiles; u16 128x512 with 1024 threads (128 KiB of LDS,
-#define BM_PK16_TB 512  // 256-B source x 1-KiB destination segments) +6-8% more (r01_ab_pk3.log)
-#endif
-#ifndef BM_PK16_NT
-#define BM_PK16_NT 1024
-#endif
-#ifndef BM_PK8_PIPE
-// packed transposes, software-pipelined blocks (k_transpose_pkp), this many
-// per CU (0 = off): uint8 .T +9.8%; uint16 +1-2% on .T but -3% on a 2-D
-// transpose, so off (profiles/r02_ab_pkpipe.log)
-#define BM_PK8_PIPE 1
-#endif
-#ifndef BM_PK16_PIPE
-#define BM_PK16_PIPE 0
-#endif
-#ifndef BM_PK8_TA
-#define BM_PK8_TA 128
-#define BM_PK8_TB 512
-#endif
-#ifndef BM_PK8_NT
-#define BM_PK8_NT 1024
-#endif
-#ifndef BM_RC_XCD
-#define BM_RC_XCD 0  // XCD-grouped covering grid: +5% in a C4 microbench (r01_rc1) but -3..-20% in the product A/B (r01_ab_rc)
-#endif
-#ifndef BM_RC_SRC_MAXB
-#define BM_RC_SRC_MAXB 0  // rows up to this many bytes are walked in source order (A/B knob)
-#endif
-#ifndef BM_GEN_GRIDCAP
-#define BM_GEN_GRIDCAP 4096  // generic copies: grid-stride (uncapped measured -20% on reversed slices, r01_index2)
-#endif
-#ifndef BM_RC_SKEW
-#define BM_RC_SKEW 0  // rowcopy: diagonal row walk when the fastest row dim's source step is >= this many bytes (0 = off; A/B knob)
-#endif
-#ifndef BM_RC_SKEW_MAXB
-// ... and rows are at most this many bytes.  Round 3 extended the diagonal
-// tiles from 256-B to 4-KiB rows (profiles/r03k_ab_diag_c4.log,
-// r03l_ab_diag_rows.log, every placement): C4 swap (2-KiB rows) 7.40 ->
-// 6.77-6.83 ms (+8.5-9.4%), 4-KiB rows +10-11%, 1 KiB +5%, 512 B +2-3%;
-// 16-KiB rows lose 2-9% (a 16x16 tile then spans 4 MiB per side), so they
-// keep row order.
-#define BM_RC_SKEW_MAXB 4096
-#endif
-#ifndef BM_RC_DIAG
-#define BM_RC_DIAG 65536  // rowcopy: 16x16 diagonal tiles when the fastest row dim's source step is >= this many bytes (0 = off): C3 +8-9%, 64 GiB target +13-15% (profiles/r02_ab_diag.log)
-#endif
-#ifndef BM_RC_DIAG_LOG2
-#define BM_RC_DIAG_LOG2 0  // diagonal tile side 2^k (0: by row size, 8x8 up to 1 KiB rows, else 16x16; A/B knob)
-#endif
-#ifndef BM_RC_DIAG_LOG2G
-#define BM_RC_DIAG_LOG2G 0  // tile side along g as log2 (0: square, the c side; A/B knob)
-#endif
-#ifndef BM_RC_DIAG_GFAST
-// rowcopy Diag16 tile order: 1 = the g-tiles (the next-fastest row dim, e.g.
-// C3's k, 128-B source step) vary fastest between consecutive tiles, so the
-// tiles resident at once read every g instead of the same 16; 0 = the c-tiles
-// (the fastest row dim).  g-fastest measured -6..-11% on the C3 / 64 GiB
-// target swaps (profiles/r03b_ab_diag.log): c-fastest stays.  A/B knob.
-#define BM_RC_DIAG_GFAST 0
-#endif
-#ifndef BM_TR_SKEW
-#define BM_TR_SKEW 0  // transpose: diagonal tile walk when the fastest batch dim's source step is >= this (0 = off; A/B knob)
-#endif
-#ifndef BM_TR_PAGEORDER
-#define BM_TR_PAGEORDER 0  // transpose: batch dims ordered by max(|src stride|, |dst stride|), smallest fastest (A/B knob)
-#endif
-#ifndef BM_TR_ROT
-// transpose: rotate each a-row of tiles by its a-tile index, so a partial last
-// b-tile (C2: 2000 = 7 x 256 + 208) is not always dispatched to the same XCD
-// (round-robin dispatch: block t runs on XCD t % 8, and with 8 b-tiles the
-// b-tile index IS the XCD).  Same tiles per group of blocks, same locality.
-#define BM_TR_ROT 0
-#endif
-#ifndef BM_TR_XCD
-#define BM_TR_XCD 0  // transpose: the blocks one XCD runs take a contiguous eighth of the tiles (A/B knob)
-#endif
-#ifndef BM_TR_ASPREAD
-// fused transposes (short source-contiguous axis fused with its continuation,
-// C3's .T): the a-tiles of consecutive tiles are spread S ways over the fused
-// source rows (ta -> (ta % S) * (ntA / S) + ta / S) when ntA >= 2 S.  A/B on
-// six placements (profiles/r03q_ab_asp_c3full.log): C3 .T S = 32 +0.7..+2.0%
-// at full size, +4.2..+5.5% at 1024 rows; S = 16 / 64 smaller or mixed.  The
-// unfused C2 swap loses 12-23% with any S (r03q_ab_asp_c2_c3.log): its tiles
-// in flight share DRAM pages of one contiguous window, so it stays in order.
-#define BM_TR_ASPREAD 32
-#endif
-#ifndef BM_TR_AROT
-// transpose, staggered order: tile (ta, tb) takes a-tile (ta + tb * ntA /
-// (ntB * BM_TR_AROT)) mod ntA, so the b-tiles in flight together (one per XCD
-// on C2) read their source rows at offsets 1/ntB of a row apart while each
-// keeps a contiguous window.  It runs only under BM_TR_AROT_FORCE: it was
-// faster on some buffers and slower on others (profiles/r03t_ab_arot*.log),
-// and the round-3 per-buffer tuner never picked it on the driver's box.
-#define BM_TR_AROT 1
-#endif
-#ifndef BM_TR_AROT_DELTA
-#define BM_TR_AROT_DELTA 0  // extra a-tiles of stagger per b-tile (A/B knob)
-#endif
-#ifndef BM_TR_AROT_FUSED
-#define BM_TR_AROT_FUSED 0  // 1: fused transposes take part too (A/B knob)
-#endif
-#ifndef BM_TR_AROT_FORCE
-#define BM_TR_AROT_FORCE 0  // 1: the staggered order (A/B knob)
-#endif
-#ifndef BM_TR_LOOP
-#define BM_TR_LOOP 0  // transpose: each block walks the batch dim that is page-local on both sides, if >= this many blocks remain (0 = off; A/B knob)
-#endif
-#ifndef BM_FUSE
-#define BM_FUSE 1  // fuse short contiguous transpose axes with their continuation (A/B knob)
-#endif
-#ifndef BM_RUNS_T
-#define BM_RUNS_T 1
-#endif
-#ifndef BM_RUNS_MAXB
-#define BM_RUNS_MAXB 64  // A/B (profiles/r01_ab5): +35% at 32-B runs, +4% at 64 B, even at 128 B
-#endif
-constexpr int kRcThreads = BM_RC_THREADS;
+// Shipped parameters (the A/B runs that chose them are in docs/HISTORY.md;
+// the rejected variants live in git history and tools/microbench/).
+// rowcopy: one 16-B vector per lane, a block per 256 vectors, up to the 2^32
+// thread launch limit (profiles/r01_ab3..ab5: many blocks +15-25% on C3/C4 swaps)
+constexpr int kRcThreads = 256;
+constexpr int kUnroll = 1;
+constexpr uint64_t kRcGridCap = 16777208;
+// rowcopy diagonal tiles (Diag16 below) when the fastest row dim steps the
+// source by >= kDiagMinStep bytes (C3 +8-9%, 64 GiB target +13-15%,
+// profiles/r02_ab_diag.log) and rows are at most kDiagMaxRow bytes: round 3
+// extended them from 256-B to 4-KiB rows (C4 swap, 2-KiB rows, +8.5-9.4%;
+// 4-KiB rows +10-11%; 16-KiB rows lose 2-9%, a 16x16 tile then spans 4 MiB
+// per side; profiles/r03k_ab_diag_c4.log, r03l_ab_diag_rows.log)
+constexpr int64_t kDiagMinStep = 65536;
+constexpr int64_t kDiagMaxRow = 4096;
+// packed-word tiles for 1-/2-byte transposes (profiles/r01_ab_pk2.log: u16
+// 128x256 +9%, u8 +11% over element-wise LDS tiles; 128x512 with 1024 threads,
+// 128 KiB of LDS, +6-8% more, r01_ab_pk3.log).  uint8 runs software-pipelined
+// (k_transpose_pkp, one block per CU): +9.8% on .T; uint16 gains 1-2% on .T
+// but loses 3% on a 2-D transpose, so it stays unpipelined (r02_ab_pkpipe.log)
+constexpr int kPkTA = 128, kPkTB = 512, kPkThreads = 1024;
+// generic copies: grid-stride (uncapped measured -20% on reversed slices, r01_index2)
+constexpr int kGenGridCap = 4096;
+// fused transposes (a short source-contiguous axis fused with its
+// continuation, C3's .T): the a-tiles of consecutive tiles are spread S ways
+// over the fused source rows (ta -> (ta % S) * (ntA / S) + ta / S) when
+// ntA >= 2 S: C3 .T +0.7..+2.0% at full size, +4.2..+5.5% at 1024 rows on six
+// placements (profiles/r03q_ab_asp_c3full.log); the unfused C2 swap loses
+// 12-23% with any S (its tiles in flight share DRAM pages of one window)
+constexpr int kASpread = 32;
+// runs transpose for kept inner runs of 32..kRunsMaxBytes bytes
+// (profiles/r01_ab5: +35% at 32-B runs, +4% at 64 B, even at 128 B)
+constexpr int64_t kRunsMaxBytes = 64;
 // HIP launch limit: grid * block threads < 2^32
 constexpr uint64_t kMaxGrid = 0xffffffffull / 1024;
-constexpr int kUnroll = BM_RC_UNROLL;
 
 // ---------------------------------------------------------------- rowcopy --
 // 16x16 diagonal tiles over the two fastest row dims (c fastest, g next, in
@@ -188,14 +88,10 @@ __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   const int L = t.lg, LG = t.lgg;
   const uint64_t D = 1ull << L, DG = 1ull << LG;
   const uint64_t tile = q >> (L + LG), w = q & (D * DG - 1);
-  uint64_t gt, ct;
-  if (BM_RC_DIAG_GFAST) {
-    ct = fd_div(tile, t.ntg);
-    gt = tile - ct * t.ntg.d;
-  } else {
-    gt = fd_div(tile, t.ntc);
-    ct = tile - gt * t.ntc.d;
-  }
+  // c-tiles vary fastest between consecutive tiles (g-fastest measured
+  // -6..-11% on the C3 / 64 GiB target swaps, profiles/r03b_ab_diag.log)
+  const uint64_t gt = fd_div(tile, t.ntc);
+  const uint64_t ct = tile - gt * t.ntc.d;
   // diagonal j, position k along g: a bijection of the D x DG tile
   const uint64_t j = w >> LG, k = w & (DG - 1);
   const uint64_t g = gt * DG + k, c = ct * D + ((k + j) & (D - 1));
@@ -253,10 +149,10 @@ struct TransDesc {
   // long tile rows.
   FastDiv Lb1, La1;
   int64_t sb2, da2;
-  uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (BM_TR_XCD)
-  FastDiv asp;     // BM_TR_ASPREAD: S (1 = off)
+  uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (0 in every shipped launch)
+  FastDiv asp;     // a-tile spread S (kASpread; 1 = off)
   uint64_t aspq;   // ntA / S
-  uint64_t arot;   // BM_TR_AROT: a-tile stagger per b-tile (0 = off)
+  uint64_t arot;   // a-tile stagger per b-tile (0 in every shipped launch)
   uint64_t ntA;
 };
 
@@ -311,11 +207,7 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t rem = t - bt * d.ntAB.d;
     uint64_t ta = fd_div(rem, d.ntB);
     uint64_t tb = rem - ta * d.ntB.d;
-    if (BM_TR_ROT) {
-      tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
-      if (tb >= d.ntB.d) tb -= d.ntB.d;
-    }
-    if (BM_TR_ASPREAD && d.asp.d > 1) {
+    if (d.asp.d > 1) {
       const uint64_t hi = fd_div(ta, d.asp);
       ta = (ta - hi * d.asp.d) * d.aspq + hi;
     }
@@ -414,10 +306,6 @@ __global__ void __launch_bounds__(NT)
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
     uint64_t tb = rem - ta * d.ntB.d;
-    if (BM_TR_ROT) {
-      tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
-      if (tb >= d.ntB.d) tb -= d.ntB.d;
-    }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
@@ -617,10 +505,6 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
     uint64_t tb = rem - ta * d.ntB.d;
-    if (BM_TR_ROT) {
-      tb += ta - fd_div(ta, d.ntB) * d.ntB.d;
-      if (tb >= d.ntB.d) tb -= d.ntB.d;
-    }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * kRunTB;
@@ -692,27 +576,6 @@ bool fill_decomp(Decomp &d, const std::vector<Dim> &outer_to_inner) {
   return true;
 }
 
-// Diagonal walk (Decomp::skew) for a decomposition whose fastest dim steps
-// the source by a large power-of-two-like stride: the dim with the smallest
-// source stride is advanced together with the fastest one, so consecutive
-// work items (lanes, blocks) read -- and write -- at different low address
-// bits instead of all hitting the same L2 sets / channels.  Applied when the
-// fastest dim's source step is >= min_bytes and another dim steps less.
-void set_skew(Decomp &d, const std::vector<Dim> &outer_to_inner, int es, int64_t min_bytes) {
-  d.skew = 0;
-  const int n = (int)outer_to_inner.size();
-  if (n < 2 || min_bytes <= 0) return;
-  const Dim &f = outer_to_inner[n - 1];
-  if (f.n < 2 || std::llabs(f.ss) * es < min_bytes) return;
-  int best = -1;
-  for (int k = 0; k < n - 1; ++k) {
-    const Dim &x = outer_to_inner[k];
-    if (x.n < 2 || std::llabs(x.ss) >= std::llabs(f.ss)) continue;
-    if (best < 0 || std::llabs(x.ss) < std::llabs(outer_to_inner[best].ss)) best = k;
-  }
-  if (best >= 0) d.skew = (n - 1 - best) + 1;  // innermost-first index + 1
-}
-
 int grid_for(uint64_t work_items, uint64_t per_block, uint64_t cap = 256ull * 16) {
   uint64_t g = (work_items + per_block - 1) / per_block;
   // default cap: 256 CUs x 16 resident-ish blocks, then grid-stride
@@ -737,34 +600,26 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
       if ((x.ss * es) % VB || (x.ds * es) % VB) ok = false;
     if (ok) break;
   }
-  if (row_bytes <= BM_RC_SRC_MAXB) {
-    // walk the rows in source order: reads stream, short rows scatter on the
-    // store side (any order of the outer dims covers the same index space)
-    std::stable_sort(outer.begin(), outer.end(), [](const Dim &x, const Dim &y) {
-      return std::llabs(x.ss) > std::llabs(y.ss);
-    });
-  }
   Decomp d;
   if (!fill_decomp(d, outer)) {
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)outer.size());
     return BM_E_ARG;
   }
-  if (row_bytes <= 256) set_skew(d, outer, es, BM_RC_SKEW);  // (A/B knob, off)
   Diag16 dg{};
   {
     // 16x16 diagonal tiles when the fastest row dim steps the source by a
     // large stride and the next one by less (C3 / 64 GiB swaps: c then b)
     const int n = (int)outer.size();
-    if (BM_RC_DIAG && row_bytes <= BM_RC_SKEW_MAXB && n >= 2 && d.skew == 0) {
+    if (row_bytes <= kDiagMaxRow && n >= 2) {
       const Dim &f = outer[n - 1], &g = outer[n - 2];
       // 8x8 tiles for rows up to 1 KiB, 16x16 above (profiles/r03n_ab_diagsize.log,
       // r03o_ab_diag8_*.log: 8x8 on C3's 128-B rows +4.3-6.1% on three
       // placements, 1-KiB rows +2%, the 64 GiB target -0.4..-1.8%; on 2-4-KiB
       // rows 16x16 is equal or +1%; 32x32 loses everywhere)
-      const int lg = BM_RC_DIAG_LOG2 > 0 ? BM_RC_DIAG_LOG2 : (row_bytes <= 1024 ? 3 : 4);
-      const int lgg = BM_RC_DIAG_LOG2G > 0 ? BM_RC_DIAG_LOG2G : lg;
+      const int lg = row_bytes <= 1024 ? 3 : 4;
+      const int lgg = lg;  // square tiles
       const int64_t D = (int64_t)1 << lg, DG = (int64_t)1 << lgg;
-      if (f.n % D == 0 && g.n % DG == 0 && std::llabs(f.ss) * es >= BM_RC_DIAG &&
+      if (f.n % D == 0 && g.n % DG == 0 && std::llabs(f.ss) * es >= kDiagMinStep &&
           std::llabs(g.ss) < std::llabs(f.ss)) {
         dg.on = 1;
         dg.lg = lg;
@@ -783,15 +638,10 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   const FastDiv fv = make_fastdiv(vpr);
   const uint64_t per = (uint64_t)kRcThreads * kUnroll;
   const uint64_t need = (total + per - 1) / per;
-  int grid, xcd = 0;
-  if (BM_RC_XCD && need >= 64 && need <= BM_RC_GRIDCAP) {
-    grid = (int)((need + 7) / 8 * 8);
-    xcd = 1;
-  } else if (need <= BM_RC_GRIDCAP) {
-    grid = (int)std::max<uint64_t>(need, 1);  // one vector per lane
-  } else {
-    grid = grid_for(total, per, BM_RC_GRIDCAP);
-  }
+  // one vector per lane (an XCD-grouped covering grid measured +5% in a C4
+  // microbench but -3..-20% in the product A/B, profiles/r01_ab_rc: xcd = 0)
+  const int xcd = 0;
+  const int grid = need <= kRcGridCap ? (int)std::max<uint64_t>(need, 1) : grid_for(total, per, kRcGridCap);
   switch (VB) {
     case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
     case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
@@ -830,41 +680,19 @@ struct Tile { int ta, tb; };
 constexpr Tile kTiles1[] = {{128, 256}, {128, 128}, {64, 64}, {256, 64}, {64, 256}};
 constexpr Tile kTiles2[] = {{128, 256}, {64, 256}, {64, 64}, {128, 64}, {256, 32}, {32, 256}};
 constexpr Tile kTiles4[] = {{64, 256}, {32, 256}, {64, 64}, {64, 128}, {128, 32}, {256, 16}, {16, 256}, {32, 64}};
-#ifndef BM_T8_FUSE512
-// f64 with 512-B destination rows whose source rows are at most this many
-// bytes apart (C5 transpose(2,0,4,1,3)): fuse b with its continuation and use
-// BM_T8_FTA x BM_T8_FTB tiles, 1-KiB write segments: +5% (2.798 -> 2.657 ms);
-// with far-apart source rows (C5 .T) fusing loses 5-20% (profiles/r02_ab_f512.log)
-#define BM_T8_FUSE512 4096
-#endif
-#ifndef BM_T8_FTA
-#define BM_T8_FTA 32
-#endif
-#ifndef BM_T8_FTB
-#define BM_T8_FTB 128
-#endif
-#ifndef BM_T8_FUSEA
-#define BM_T8_FUSEA 0  // f64 with 512-B source rows far apart (C5 .T): fuse a with its source continuation, BM_T8_FATA x BM_T8_FATB tiles (A/B knob)
-#endif
-#ifndef BM_T8_FATA
-#define BM_T8_FATA 128
-#endif
-#ifndef BM_T8_FATB
-#define BM_T8_FATB 64
-#endif
-#ifndef BM_T8_SQUARE
-#define BM_T8_SQUARE 0  // f64: 64x64 tiles ahead of 32x64 on equal cost (512-B source segments; A/B knob)
-#endif
-#if BM_T8_SQUARE
-constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {64, 64}, {32, 64}, {64, 32}, {128, 16}, {16, 128}};
-#else
+// f64 with 512-B destination rows whose source rows are at most
+// kT8Fuse512 bytes apart (C5 transpose(2,0,4,1,3)): fuse b with its
+// continuation and use 32 x 128 tiles, 1-KiB write segments: +5% (2.798 ->
+// 2.657 ms); with far-apart source rows (C5 .T) fusing loses 5-20%
+// (profiles/r02_ab_f512.log)
+constexpr int64_t kT8Fuse512 = 4096;
+constexpr Tile kT8FusedTile = {32, 128};
 constexpr Tile kTiles8[] = {{32, 256}, {16, 256}, {32, 64}, {64, 64}, {64, 32}, {128, 16}, {16, 128}};
-#endif
 
 template <typename T>
 int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool va_vec, bool vb_vec,
-                       bool fused, hipStream_t st, uint64_t loop_n = 1) {
-  uint64_t g = td.ntiles / loop_n;
+                       bool fused, hipStream_t st) {
+  uint64_t g = td.ntiles;
   if (g > kMaxGrid) g = kMaxGrid;  // grid-stride beyond the launch limit
   const int grid = (int)g;
 #define BM_TILE(A, B) \
@@ -879,12 +707,7 @@ int launch_transpose_t(const T *src, T *dst, const TransDesc &td, Tile tl, bool 
   } else {
     BM_TILE(32, 256) BM_TILE(16, 256) BM_TILE(32, 64) BM_TILE(64, 64) BM_TILE(64, 32) BM_TILE(128, 16)
     BM_TILE(16, 128)
-#if BM_T8_FUSE512
-    BM_TILE(BM_T8_FTA, BM_T8_FTB)
-#endif
-#if BM_T8_FUSEA
-    BM_TILE(BM_T8_FATA, BM_T8_FATB)
-#endif
+    BM_TILE(kT8FusedTile.ta, kT8FusedTile.tb)
   }
 #undef BM_TILE
   bm_set_error("bm_copy_strided: no transpose tile %dx%d for %d-byte elements", tl.ta, tl.tb, (int)sizeof(T));
@@ -940,14 +763,14 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   // destination (ds == Lb) and a with the dim that continues it in the source
   // (ss == La), so tile rows stay >= 512 B / 256 B (C3 .T: 128-B source rows,
   // +21%, profiles/r01_ab_fuse.log).
-  bool fused = false, fused512 = false, fusedA = false;
-  if (BM_FUSE && allow_fuse && es >= 4 && aligned(src, 16) && aligned(dst, 16)) {
+  bool fused = false, fused512 = false;
+  if (allow_fuse && es >= 4 && aligned(src, 16) && aligned(dst, 16)) {
     auto take = [&](bool want_b) -> int {
       for (int k = 0; k < (int)batch.size(); ++k)
         if (want_b ? batch[k].ds == td.Lb : batch[k].ss == td.La) return k;
       return -1;
     };
-    const bool f512 = BM_T8_FUSE512 && es == 8 && td.Lb * es == 512 && std::llabs(td.sb) * es <= BM_T8_FUSE512;
+    const bool f512 = es == 8 && td.Lb * es == 512 && std::llabs(td.sb) * es <= kT8Fuse512;
     if (td.Lb * es < 512 || f512) {
       const int k = take(true);
       if (k >= 0) {
@@ -958,11 +781,9 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
         fused = true;
       }
     }
-    const bool fa = BM_T8_FUSEA && es == 8 && td.La * es == 512 && std::llabs(td.sb) * es > 4096 && !fused;
-    if (td.La * es < 256 || fa) {
+    if (td.La * es < 256) {
       const int k = take(false);
       if (k >= 0) {
-        fusedA = fa;
         td.da2 = batch[k].ds;
         td.La *= batch[k].n;
         batch.erase(batch.begin() + k);
@@ -970,58 +791,29 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
       }
     }
   }
-  if (BM_TR_PAGEORDER) {
-    // consecutive tiles step the batch dim with the smallest larger-of-the-two
-    // strides, so they stay inside the same source AND destination pages
-    // (C5 .T: i2, 32 KiB on both sides, instead of i1: 2 MiB in the source;
-    // the UTCL1 misses of profiles/r02_kernel_counters.md)
-    std::stable_sort(batch.begin(), batch.end(), [](const Dim &x, const Dim &y) {
-      return std::max(std::llabs(x.ss), std::llabs(x.ds)) > std::max(std::llabs(y.ss), std::llabs(y.ds));
-    });
-  }
   Tile tl = pick_tile(td.La, td.Lb, es);
-  if (fused512) tl = Tile{BM_T8_FTA, BM_T8_FTB};
-  if (fusedA) tl = Tile{BM_T8_FATA, BM_T8_FATB};
+  if (fused512) tl = kT8FusedTile;
   const int TA = tl.ta, TB = tl.tb;
   const uint64_t ntA = (uint64_t)((td.La + TA - 1) / TA);
   const uint64_t ntB = (uint64_t)((td.Lb + TB - 1) / TB);
   uint64_t nb = 1;
   for (const Dim &x : batch) nb *= (uint64_t)x.n;
-  // Each block walks the batch dim whose source AND destination strides are
-  // smallest (C5 .T: i2, 32 KiB on both sides): its tiles then stay inside the
-  // same source and destination pages (UTCL1 misses, profiles/
-  // r02_kernel_counters.md).  The dim becomes the slowest of the tile index
-  // and the grid covers the rest, so the grid-stride loop steps it.
-  uint64_t loop_n = 1;
-  if (BM_TR_LOOP && !batch.empty()) {
-    int best = -1;
-    int64_t best_m = 0;
-    for (int k = 0; k < (int)batch.size(); ++k) {
-      const int64_t m = std::max(std::llabs(batch[k].ss), std::llabs(batch[k].ds));
-      if (batch[k].n >= 8 && (best < 0 || m < best_m)) best = k, best_m = m;
-    }
-    if (best >= 0 && best_m * es <= 65536 && ntA * ntB * (nb / (uint64_t)batch[best].n) >= (uint64_t)BM_TR_LOOP) {
-      loop_n = (uint64_t)batch[best].n;
-      std::rotate(batch.begin(), batch.begin() + best, batch.begin() + best + 1);
-    }
-  }
   if (!fill_decomp(td.batch, batch)) {
     bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)batch.size());
     return BM_E_ARG;
   }
-  set_skew(td.batch, batch, es, BM_TR_SKEW);
   td.ntB = make_fastdiv(ntB);
   td.ntAB = make_fastdiv(ntA * ntB);
   td.ntiles = ntA * ntB * nb;
   td.asp = make_fastdiv(1);
   td.aspq = ntA;
   td.ntA = ntA;
-  td.arot = 0;  // in-order walk (the staggered order is an A/B knob, below)
-  if (BM_TR_ASPREAD > 1 && fused && ntA % BM_TR_ASPREAD == 0 && ntA >= 2 * BM_TR_ASPREAD) {
-    td.asp = make_fastdiv(BM_TR_ASPREAD);
-    td.aspq = ntA / BM_TR_ASPREAD;
+  td.arot = 0;  // in-order walk
+  td.xcd8 = 0;
+  if (fused && ntA % kASpread == 0 && ntA >= 2 * kASpread) {
+    td.asp = make_fastdiv(kASpread);
+    td.aspq = ntA / kASpread;
   }
-  td.xcd8 = (BM_TR_XCD && td.ntiles % 8 == 0 && td.ntiles / loop_n <= kMaxGrid && loop_n == 1) ? td.ntiles / 8 : 0;
   // 16-B vectors when every source row start (dims other than a) and every
   // destination row start (dims other than b) is 16-B aligned.
   bool va = aligned(src, 16), vb = aligned(dst, 16);
@@ -1033,45 +825,31 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
     // the fused kernels are vectorised only: the plain tiles handle it
     return launch_transpose(src, dst, dims, a, es, st, false);
   }
-  if (BM_PK && va && vb && (es == 1 || es == 2)) {
-    // packed-word tiles: 128-B source and 1-KiB destination segments
-    const int ta = es == 2 ? BM_PK16_TA : BM_PK8_TA, tbb = es == 2 ? BM_PK16_TB : BM_PK8_TB;
+  if (va && vb && (es == 1 || es == 2)) {
+    // packed-word tiles: 256-B (u16) / 128-B (u8) source and 1-KiB destination segments
     TransDesc tp = td;
-    const uint64_t pA = (uint64_t)((td.La + ta - 1) / ta), pB = (uint64_t)((td.Lb + tbb - 1) / tbb);
+    const uint64_t pA = (uint64_t)((td.La + kPkTA - 1) / kPkTA), pB = (uint64_t)((td.Lb + kPkTB - 1) / kPkTB);
     tp.ntB = make_fastdiv(pB);
     tp.ntAB = make_fastdiv(pA * pB);
     tp.ntiles = pA * pB * nb;
-    uint64_t g = tp.ntiles / loop_n;
+    uint64_t g = tp.ntiles;
     if (g > kMaxGrid) g = kMaxGrid;
-    const int pipe = es == 2 ? BM_PK16_PIPE : BM_PK8_PIPE;
-    if (pipe) {
-      const uint64_t cap = 256ull * pipe;  // MI355X: 256 CUs
-      if (g > cap) g = cap;
-      if (es == 2)
-        k_transpose_pkp<uint16_t, BM_PK16_TA, BM_PK16_TB, BM_PK16_NT><<<(int)g, BM_PK16_NT, 0, st>>>(
-            (const uint16_t *)src, (uint16_t *)dst, tp);
-      else
-        k_transpose_pkp<uint8_t, BM_PK8_TA, BM_PK8_TB, BM_PK8_NT><<<(int)g, BM_PK8_NT, 0, st>>>(
-            (const uint8_t *)src, (uint8_t *)dst, tp);
-      return BM_OK;
+    if (es == 2) {
+      k_transpose_pk<uint16_t, kPkTA, kPkTB, kPkThreads><<<(int)g, kPkThreads, 0, st>>>((const uint16_t *)src,
+                                                                                     (uint16_t *)dst, tp);
+    } else {
+      if (g > 256) g = 256;  // pipelined: one block per CU (MI355X: 256 CUs)
+      k_transpose_pkp<uint8_t, kPkTA, kPkTB, kPkThreads><<<(int)g, kPkThreads, 0, st>>>((const uint8_t *)src,
+                                                                                      (uint8_t *)dst, tp);
     }
-    if (es == 2)
-      k_transpose_pk<uint16_t, BM_PK16_TA, BM_PK16_TB, BM_PK16_NT><<<(int)g, BM_PK16_NT, 0, st>>>((const uint16_t *)src,
-                                                                                 (uint16_t *)dst, tp);
-    else
-      k_transpose_pk<uint8_t, BM_PK8_TA, BM_PK8_TB, BM_PK8_NT><<<(int)g, BM_PK8_NT, 0, st>>>((const uint8_t *)src,
-                                                                              (uint8_t *)dst, tp);
     return BM_OK;
   }
-  if (BM_TR_AROT_FORCE && BM_TR_AROT && (!fused || BM_TR_AROT_FUSED) && ntB > 1 && ntA >= ntB * BM_TR_AROT &&
-      loop_n == 1 && !td.xcd8)
-    td.arot = (ntA / (ntB * BM_TR_AROT) + BM_TR_AROT_DELTA) % ntA;  // staggered order (A/B knob)
   int rc = BM_E_ARG;
   switch (es) {
-    case 1: rc = launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, false, st, loop_n); break;
-    case 2: rc = launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, false, st, loop_n); break;
-    case 4: rc = launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, fused, st, loop_n); break;
-    case 8: rc = launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, fused, st, loop_n); break;
+    case 1: rc = launch_transpose_t<uint8_t>((const uint8_t *)src, (uint8_t *)dst, td, tl, va, vb, false, st); break;
+    case 2: rc = launch_transpose_t<uint16_t>((const uint16_t *)src, (uint16_t *)dst, td, tl, va, vb, false, st); break;
+    case 4: rc = launch_transpose_t<uint32_t>((const uint32_t *)src, (uint32_t *)dst, td, tl, va, vb, fused, st); break;
+    case 8: rc = launch_transpose_t<uint64_t>((const uint64_t *)src, (uint64_t *)dst, td, tl, va, vb, fused, st); break;
     default: bm_set_error("bm_copy_strided: transpose with elem_bytes %d", es);
   }
   return rc;
@@ -1086,7 +864,7 @@ int launch_generic(const char *src, char *dst, const std::vector<Dim> &dims, int
   }
   uint64_t total = 1;
   for (const Dim &x : dims) total *= (uint64_t)x.n;
-  const int grid = grid_for(total, kThreads, BM_GEN_GRIDCAP);
+  const int grid = grid_for(total, kThreads, kGenGridCap);
   switch (es) {
     case 1: k_generic<1><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
     case 2: k_generic<2><<<grid, kThreads, 0, st>>>(src, dst, d, total); break;
@@ -1110,7 +888,7 @@ int try_transpose_runs(const char *src, char *dst, const std::vector<Dim> &dims,
   if (n < 3) return 1;
   const Dim &in = dims.back();
   const int64_t rb = in.n * es;
-  if (rb % 16 || rb < 32 || rb > BM_RUNS_MAXB) return 1;
+  if (rb % 16 || rb < 32 || rb > kRunsMaxBytes) return 1;
   if (!aligned(src, 16) || !aligned(dst, 16)) return 1;
   const int B = n - 2;
   if (dims[B].ds != in.n) return 1;
@@ -1213,8 +991,7 @@ extern "C" int bm_copy_strided(const void *src_, void *dst_, int ndim, const int
   int rc;
   const Dim &in = c.back();
   if (in.ss == 1 && in.ds == 1) {
-    rc = (BM_RUNS_T && try_transpose_runs(src, dst, c, es, st) == 0) ? BM_OK
-                                                                    : launch_rowcopy(src, dst, c, es, st);
+    rc = try_transpose_runs(src, dst, c, es, st) == 0 ? BM_OK : launch_rowcopy(src, dst, c, es, st);
   } else {
     int a = -1;
     if (in.ds == 1 && es <= 8)
