@@ -393,7 +393,13 @@ __global__ void __launch_bounds__(kCThreads)
         int64_t k = (int64_t)((double)off * inv[lo]);
         if (k * len > off) --k;
         else if ((k + 1) * len <= off) ++k;
-        const V *sp = s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + (off - k * len);
+        // a table that does not tile the records (a wrong BM_RUNS_TILED) gives
+        // wrong bytes, never an access outside run b of a source record of
+        // this group: k in [0, group), the offset in [0, len)
+        k = k < 0 ? 0 : (k >= group ? group - 1 : k);
+        int64_t w = off - k * len;
+        w = w < 0 ? 0 : (w >= len ? len - 1 : w);
+        const V *sp = s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + w;
         x[u] = *sp;  // temporal: the shared line's second read hits L2
       }
     }

@@ -50,11 +50,7 @@ __host__ __device__ __forceinline__ uint64_t fd_div(uint64_t n, const FastDiv &f
 // stored innermost first; accumulates source and destination offsets.
 struct Decomp {
   int32_t n;
-  // skew: 0 = none; k + 1 = coordinate k (innermost-first) is replaced by
-  // (x_k + x_0) mod n_k -- a bijection that makes consecutive indices step
-  // dim 0 and dim k together (a diagonal walk), so that consecutive work
-  // items do not share the low address bits of a power-of-two stride
-  int32_t skew;
+  int32_t pad_;
   FastDiv div[BM_MAXD];
   int64_t ss[BM_MAXD];
   int64_t ds[BM_MAXD];
@@ -65,25 +61,14 @@ __device__ __forceinline__ void decomp2(uint64_t idx, const Decomp &d, int64_t &
   so = 0;
   dof = 0;
   const int n = d.n;
-  const int sk = d.skew - 1;
-  uint64_t r0 = 0;
   for (int k = 0; k + 1 < n; ++k) {
-    uint64_t q = fd_div(idx, d.div[k]);
-    uint64_t r = idx - q * d.div[k].d;
-    if (k == 0) r0 = r;
-    if (k == sk) {
-      const uint64_t t = r + r0;
-      r = t - fd_div(t, d.div[k]) * d.div[k].d;
-    }
+    const uint64_t q = fd_div(idx, d.div[k]);
+    const uint64_t r = idx - q * d.div[k].d;
     so += (int64_t)r * d.ss[k];
     dof += (int64_t)r * d.ds[k];
     idx = q;
   }
   if (n > 0) {  // outermost: the remaining index is the coordinate
-    if (n - 1 == sk) {
-      const uint64_t t = idx + r0;
-      idx = t - fd_div(t, d.div[n - 1]) * d.div[n - 1].d;
-    }
     so += (int64_t)idx * d.ss[n - 1];
     dof += (int64_t)idx * d.ds[n - 1];
   }

@@ -74,41 +74,35 @@ constexpr uint64_t kMaxGrid = 0xffffffffull / 1024;
 // (tools/skew/rowcopy_skew.hip "diag16").  A bijection inside each tile.
 struct Diag16 {
   int on;
-  int lg;        // log2 of the tile side along c (3: 8, 4: 16)
-  int lgg;       // log2 of the tile side along g (= lg for square tiles)
+  int lg;        // log2 of the (square) tile side (3: 8, 4: 16)
   FastDiv grp;   // Ng * Nc rows per (outer) group
-  FastDiv ntc;   // Nc / 16 tiles along c
-  FastDiv ntg;   // Ng / 16 tiles along g
+  FastDiv ntc;   // Nc / D tiles along c
   uint64_t nc;   // Nc
 };
 
 __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   const uint64_t outer = fd_div(row, t.grp);
   const uint64_t q = row - outer * t.grp.d;
-  const int L = t.lg, LG = t.lgg;
-  const uint64_t D = 1ull << L, DG = 1ull << LG;
-  const uint64_t tile = q >> (L + LG), w = q & (D * DG - 1);
+  const int L = t.lg;
+  const uint64_t D = 1ull << L;
+  const uint64_t tile = q >> (2 * L), w = q & (D * D - 1);
   // c-tiles vary fastest between consecutive tiles (g-fastest measured
   // -6..-11% on the C3 / 64 GiB target swaps, profiles/r03b_ab_diag.log)
   const uint64_t gt = fd_div(tile, t.ntc);
   const uint64_t ct = tile - gt * t.ntc.d;
-  // diagonal j, position k along g: a bijection of the D x DG tile
-  const uint64_t j = w >> LG, k = w & (DG - 1);
-  const uint64_t g = gt * DG + k, c = ct * D + ((k + j) & (D - 1));
+  // diagonal j, position k along g: a bijection of the D x D tile
+  const uint64_t j = w >> L, k = w & (D - 1);
+  const uint64_t g = gt * D + k, c = ct * D + ((k + j) & (D - 1));
   return outer * t.grp.d + g * t.nc + c;
 }
 
 template <int VB>
 __global__ void __launch_bounds__(kRcThreads)
     k_rowcopy(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
-              FastDiv vpr, uint64_t total, int es, int xcd, Diag16 dg) {
+              FastDiv vpr, uint64_t total, int es, Diag16 dg) {
   typedef typename VecB<VB>::t V;
   const uint64_t step = (uint64_t)gridDim.x * kRcThreads * kUnroll;
-  // xcd: the grid covers the copy (a multiple of 8 blocks); blocks dealt to
-  // XCD x (b % 8 under round-robin dispatch) take the x-th contiguous eighth
-  uint64_t bid = blockIdx.x;
-  if (xcd) bid = (bid % 8) * (gridDim.x / 8) + bid / 8;
-  for (uint64_t base = bid * kRcThreads * kUnroll + threadIdx.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * kRcThreads * kUnroll + threadIdx.x;
        base < total; base += step) {
     V reg[kUnroll];
     int64_t doff[kUnroll];
@@ -149,11 +143,8 @@ struct TransDesc {
   // long tile rows.
   FastDiv Lb1, La1;
   int64_t sb2, da2;
-  uint64_t xcd8;   // != 0: tiles / 8, and block b takes tile (b % 8) * xcd8 + b / 8 (0 in every shipped launch)
   FastDiv asp;     // a-tile spread S (kASpread; 1 = off)
   uint64_t aspq;   // ntA / S
-  uint64_t arot;   // a-tile stagger per b-tile (0 in every shipped launch)
-  uint64_t ntA;
 };
 
 // TA x TB tile (TA along a, the source-contiguous dim; TB along b, the
@@ -199,10 +190,9 @@ __global__ void __launch_bounds__(kThreads)
   const int ia = tx * VA;
   const int ib = ux * VB;
 
-  for (uint64_t t0 = blockIdx.x; t0 < d.ntiles; t0 += gridDim.x) {
+  for (uint64_t t = blockIdx.x; t < d.ntiles; t += gridDim.x) {
     // consecutive blocks walk dim b (the destination-contiguous one): their
     // stores land side by side in the same destination rows (+9% measured)
-    const uint64_t t = d.xcd8 ? (t0 % 8) * d.xcd8 + t0 / 8 : t0;
     const uint64_t bt = fd_div(t, d.ntAB);
     const uint64_t rem = t - bt * d.ntAB.d;
     uint64_t ta = fd_div(rem, d.ntB);
@@ -210,10 +200,6 @@ __global__ void __launch_bounds__(kThreads)
     if (d.asp.d > 1) {
       const uint64_t hi = fd_div(ta, d.asp);
       ta = (ta - hi * d.asp.d) * d.aspq + hi;
-    }
-    if (d.arot) {
-      ta += tb * d.arot;
-      while (ta >= d.ntA) ta -= d.ntA;
     }
     int64_t so, dof;
     decomp2(bt, d.batch, so, dof);
@@ -561,7 +547,7 @@ bool fill_decomp(Decomp &d, const std::vector<Dim> &outer_to_inner) {
   const int n = (int)outer_to_inner.size();
   if (n > BM_MAXD) return false;
   d.n = n;
-  d.skew = 0;
+  d.pad_ = 0;
   for (int k = 0; k < n; ++k) {  // store innermost first
     const Dim &x = outer_to_inner[n - 1 - k];
     d.div[k] = make_fastdiv((uint64_t)x.n);
@@ -617,16 +603,13 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
       // placements, 1-KiB rows +2%, the 64 GiB target -0.4..-1.8%; on 2-4-KiB
       // rows 16x16 is equal or +1%; 32x32 loses everywhere)
       const int lg = row_bytes <= 1024 ? 3 : 4;
-      const int lgg = lg;  // square tiles
-      const int64_t D = (int64_t)1 << lg, DG = (int64_t)1 << lgg;
-      if (f.n % D == 0 && g.n % DG == 0 && std::llabs(f.ss) * es >= kDiagMinStep &&
+      const int64_t D = (int64_t)1 << lg;
+      if (f.n % D == 0 && g.n % D == 0 && std::llabs(f.ss) * es >= kDiagMinStep &&
           std::llabs(g.ss) < std::llabs(f.ss)) {
         dg.on = 1;
         dg.lg = lg;
-        dg.lgg = lgg;
         dg.grp = make_fastdiv((uint64_t)(f.n * g.n));
         dg.ntc = make_fastdiv((uint64_t)(f.n / D));
-        dg.ntg = make_fastdiv((uint64_t)(g.n / DG));
         dg.nc = (uint64_t)f.n;
       }
     }
@@ -639,15 +622,14 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   const uint64_t per = (uint64_t)kRcThreads * kUnroll;
   const uint64_t need = (total + per - 1) / per;
   // one vector per lane (an XCD-grouped covering grid measured +5% in a C4
-  // microbench but -3..-20% in the product A/B, profiles/r01_ab_rc: xcd = 0)
-  const int xcd = 0;
+  // microbench but -3..-20% in the product A/B, profiles/r01_ab_rc)
   const int grid = need <= kRcGridCap ? (int)std::max<uint64_t>(need, 1) : grid_for(total, per, kRcGridCap);
   switch (VB) {
-    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
-    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
-    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
-    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
-    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, xcd, dg); break;
+    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
+    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
+    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
+    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
+    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
   }
   return BM_OK;
 }
@@ -807,9 +789,6 @@ int launch_transpose(const char *src, char *dst, const std::vector<Dim> &dims, i
   td.ntiles = ntA * ntB * nb;
   td.asp = make_fastdiv(1);
   td.aspq = ntA;
-  td.ntA = ntA;
-  td.arot = 0;  // in-order walk
-  td.xcd8 = 0;
   if (fused && ntA % kASpread == 0 && ntA >= 2 * kASpread) {
     td.asp = make_fastdiv(kASpread);
     td.aspq = ntA / kASpread;

@@ -240,22 +240,32 @@ def gather_to_host(ctx, local, sizes, out=None):
     window (EGRESS_WINDOW).  ``out``: a host uint8 array to fill instead."""
     from bolt_amd.mi355x.transfer import copy_to_host
     sizes = [int(v) for v in sizes]
-    total = sum(sizes)
     if out is None:
-        out = np.empty(total, dtype=np.uint8)
+        out = np.empty(sum(sizes), dtype=np.uint8)
     if ctx.world_size == 1:
         copy_to_host(local, out)
         return out
+    return gather_windows(ctx, local, sizes, out, all_gather_bytes)
+
+
+def gather_windows(ctx, local, sizes, out, gather):
+    """gather_to_host's windows: each window of the global byte sequence is one
+    ``gather`` (all_gather_bytes) into a window-sized device buffer, then a
+    staged D2H into its place in ``out``; the two page-locked staging buffers
+    are allocated once for all windows."""
+    from bolt_amd.mi355x.transfer import SMALL, copy_to_host, staging_buffers
+    total = sum(sizes)
     offs = np.r_[0, np.cumsum(sizes)].astype(np.int64)
     me = ctx.rank
     w = max(1, egress_window())
+    staging = staging_buffers() if local.device.type == "cuda" and min(w, total) > SMALL else None
     for g0 in range(0, total, w):
         g1 = min(total, g0 + w)
-        part = [max(0, min(g1, int(offs[r + 1])) - max(g0, int(offs[r]))) for r in range(ctx.world_size)]
+        part = [max(0, min(g1, int(offs[r + 1])) - max(g0, int(offs[r]))) for r in range(len(sizes))]
         lo = max(g0, int(offs[me])) - int(offs[me])
         piece = local[lo:lo + part[me]] if part[me] else local[:0]
-        buf = all_gather_bytes(ctx, piece, part)
-        copy_to_host(buf, out[g0:g1])
+        buf = gather(ctx, piece, part)
+        copy_to_host(buf, out[g0:g1], staging)
         del buf
     return out
 
@@ -339,20 +349,37 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
     out = _empty(int(np.prod(loc_out)) * es, data.device)
     tstr = contiguous_strides(loc_out)
     sstr = [sin[p] for p in perm]
-    # Pipeline the exchange in K stages along the output rows: stage k packs
-    # its sub-blocks, starts its all-to-all asynchronously (RCCL stream) and,
-    # while that runs, the current stream unpacks stage k-1 and packs k+1.
+    # Pipeline the exchange in K stages: stage k packs its sub-blocks, starts
+    # its all-to-all asynchronously (RCCL stream) and, while that runs, the
+    # current stream unpacks stage k-1 and packs k+1.  The stages split the
+    # output's leading axis (every peer's rows in K parts) -- unless that axis
+    # is the source-contiguous one (a .T: C3 / C5), whose rows per peer and
+    # stage would be a few elements (16-B source segments, 0.11 of HBM peak in
+    # the r05a rehearsal): the stages then split the largest other output axis
+    # that is not the exchanged one, and each pack reads whole source rows.
+    stage_ax = None
+    if sin[a] == 1 and nd >= 3:
+        cand = [k for k in range(1, nd) if k != j and out_shape[k] > 1]
+        if cand:
+            stage_ax = max(cand, key=lambda k: (out_shape[k], -k))
     # K must agree on every rank (each stage is one collective), so it comes
     # from global quantities only: the largest slab's per-peer block
     max_rows = max(hi_ - lo_ for lo_, hi_ in in_b)
     per_peer = max_rows * int(np.prod(shape[1:])) * es // G
     K = STAGES if STAGES else int(max(1, min(8, per_peer // stage_bytes(G))))
-    K = max(1, min(K, min(b - a_ for a_, b in out_b) or 1))
+    if stage_ax is None:
+        K = max(1, min(K, min(b - a_ for a_, b in out_b) or 1))
+    else:
+        K = max(1, min(K, out_shape[stage_ax]))
 
     def sub(q, k):
+        """(output rows of peer q, range of the stage axis or None) in stage k."""
         qlo, qhi = out_b[q]
-        n = qhi - qlo
-        return qlo + k * n // K, qlo + (k + 1) * n // K
+        if stage_ax is None:
+            n = qhi - qlo
+            return (qlo + k * n // K, qlo + (k + 1) * n // K), None
+        n = out_shape[stage_ax]
+        return (qlo, qhi), (k * n // K, (k + 1) * n // K)
 
     # equal slabs on every rank (the weak-scaling benches): one pack and one
     # unpack launch per stage instead of one per peer
@@ -364,41 +391,49 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
         for k in range(K):
             send_sizes, parts = [], []
             for q in range(G):
-                slo_q, shi_q = sub(q, k)
+                (slo_q, shi_q), sr = sub(q, k)
                 bshape = list(out_shape)
                 bshape[0] = shi_q - slo_q
                 bshape[j] = in_hi - in_lo
-                parts.append((slo_q, bshape))
+                off = slo_q * sin[a]                   # source element offset of the block
+                if sr is not None:
+                    bshape[stage_ax] = sr[1] - sr[0]
+                    off += sr[0] * sstr[stage_ax]
+                parts.append((off, bshape))
                 send_sizes.append(int(np.prod(bshape)) * es)
             send = _empty(sum(send_sizes), data.device)
             if even_out and send_sizes[0]:
                 # every peer's block has one shape and the sources are evenly
                 # spaced along axis a: the G packs are one strided copy
                 bshape = parts[0][1]
-                backend.copy_strided(data, parts[0][0] * sin[a] * es, send, 0, [G] + bshape,
-                                     [(parts[1][0] - parts[0][0]) * sin[a]] + sstr,
+                backend.copy_strided(data, parts[0][0] * es, send, 0, [G] + bshape,
+                                     [parts[1][0] - parts[0][0]] + sstr,
                                      [send_sizes[0] // es] + contiguous_strides(bshape), es)
             else:
                 off = 0
-                for (slo_q, bshape), nb in zip(parts, send_sizes):
+                for (soff, bshape), nb in zip(parts, send_sizes):
                     if nb:
-                        backend.copy_strided(data, slo_q * sin[a] * es, send, off, bshape, sstr,
+                        backend.copy_strided(data, soff * es, send, off, bshape, sstr,
                                              contiguous_strides(bshape), es)
                     off += nb
-            mlo, mhi = sub(r, k)
+            (mlo, mhi), sr = sub(r, k)
             recv_sizes, rparts = [], []
             for s_ in range(G):
                 slo, shi = in_b[s_]
                 bshape = list(loc_out)
                 bshape[0] = mhi - mlo
                 bshape[j] = shi - slo
-                rparts.append((slo, bshape))
+                doff = (mlo - lo) * tstr[0] + slo * tstr[j]   # destination element offset
+                if sr is not None:
+                    bshape[stage_ax] = sr[1] - sr[0]
+                    doff += sr[0] * tstr[stage_ax]
+                rparts.append((doff, bshape))
                 recv_sizes.append(int(np.prod(bshape)) * es)
             recv, work = all_to_all_bytes(ctx, send, send_sizes, recv_sizes, _unit(es), async_op=True)
             if pending is not None:
-                _unpack(backend, pending, out, tstr, j, es, even_in)
-            pending = (recv, work, send, rparts, recv_sizes, mlo - lo)
-        _unpack(backend, pending, out, tstr, j, es, even_in)
+                _unpack(backend, pending, out, tstr, es, even_in)
+            pending = (recv, work, send, rparts, recv_sizes)
+        _unpack(backend, pending, out, tstr, es, even_in)
         if ctx.transport == "rccl":
             # bounded host wait for the last exchange (the final unpack is
             # already queued behind it): a failed peer raises, never hangs
@@ -406,23 +441,22 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
     return out
 
 
-def _unpack(backend, pending, out, tstr, j, es, even=False):
-    recv, work, send, rparts, recv_sizes, row0 = pending
+def _unpack(backend, pending, out, tstr, es, even=False):
+    recv, work, send, rparts, recv_sizes = pending
     if work is not None:
         work.wait()  # the current stream waits for this stage's all-to-all
     if even and recv_sizes[0]:
         # equal blocks from every rank, landing evenly spaced along axis j: one copy
-        slo, bshape = rparts[0]
+        doff, bshape = rparts[0]
         G = len(rparts)
-        backend.copy_strided(recv, 0, out, (row0 * tstr[0] + slo * tstr[j]) * es, [G] + bshape,
+        backend.copy_strided(recv, 0, out, doff * es, [G] + bshape,
                              [recv_sizes[0] // es] + contiguous_strides(bshape),
-                             [(rparts[1][0] - slo) * tstr[j]] + tstr, es)
+                             [rparts[1][0] - doff] + tstr, es)
     else:
         off = 0
-        for (slo, bshape), nb in zip(rparts, recv_sizes):
+        for (doff, bshape), nb in zip(rparts, recv_sizes):
             if nb:
-                backend.copy_strided(recv, off, out, (row0 * tstr[0] + slo * tstr[j]) * es, bshape,
-                                     contiguous_strides(bshape), tstr, es)
+                backend.copy_strided(recv, off, out, doff * es, bshape, contiguous_strides(bshape), tstr, es)
             off += nb
     del send
 

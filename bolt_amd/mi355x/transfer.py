@@ -102,10 +102,18 @@ def to_host(t, dtype, shape):
     return out.view(dtype).reshape(shape)
 
 
-def copy_to_host(t, out):
+def staging_buffers():
+    """Two page-locked CHUNK-byte buffers for copy_to_host (a caller that copies
+    many windows allocates them once)."""
+    import torch
+    return [torch.empty(CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+
+
+def copy_to_host(t, out, staging=None):
     """out[:] = the bytes of uint8 tensor ``t`` (``out`` a host uint8 ndarray of
-    t.numel() bytes), staged through two page-locked chunks: the host copy out
-    of chunk i overlaps the DMA of chunk i+1."""
+    t.numel() bytes), staged through two page-locked chunks (``staging``, or
+    two from torch's caching host allocator): the host copy out of chunk i
+    overlaps the DMA of chunk i+1."""
     import torch
     n = t.numel()
     if n == 0:
@@ -120,7 +128,7 @@ def copy_to_host(t, out):
         stream.synchronize()
         _par_copy(out, host.numpy())
         return
-    bufs = [torch.empty(CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    bufs = staging if staging is not None else staging_buffers()
     evs = [torch.cuda.Event(), torch.cuda.Event()]
     starts = list(range(0, n, CHUNK))
     # keep one DMA in flight ahead of the host copy out of the previous chunk

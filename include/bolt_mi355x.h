@@ -227,7 +227,10 @@ int bm_record_scatter(const void *src, void *dst, int64_t nrec, int64_t src_rec,
  * flags: BM_RUNS_TILED when the runs tile every new record (m_b = len_b and
  * the regions [a_b, a_b + group * len_b), sorted by a_b, lie back to back
  * from 0 to dst_group_stride; at most 64 runs): the kernel then walks the
- * destination in order, whole lines per wave, each lane finding its source.
+ * destination in order, whole lines per wave, each lane finding its source;
+ * the flag on runs that do not tile gives wrong bytes (every read stays inside
+ * a run of a source record of the group, the runs themselves inside the
+ * records as above).  Without the flag: one wave per (record, run).
  * C5's keys_to_values((2,)): 16 chunk boxes of 2.6-3.2 KB per record
  * (bolt/spark/chunk.py:202-289).  Bit-exact.
  */

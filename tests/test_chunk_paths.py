@@ -336,3 +336,73 @@ def test_record_runs_fuzz(bctx, monkeypatch, case):
         out[runs] = (k._packed.cpu().numpy().tobytes(), k.unchunk().toarray().tobytes(), k.plan.tolist(),
                      k.padding.tolist(), k.shape)
     assert out["1"] == out["0"], (shape, split, dtype, plan, pad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+def test_record_runs_untiled_table(gpu_ctx, es):
+    """bm_record_runs WITHOUT BM_RUNS_TILED (k_record_runs: one wave per
+    (record, run)), called directly: a table whose runs leave gaps in the
+    destination, stack with a stride m != len and start mid-record, so no
+    keys_to_values reaches it.  Every destination byte equals the numpy
+    executor's (tests/cpu_backend.py) on the same bytes, gap bytes untouched;
+    every element size, 16-B vectors."""
+    import sys
+    import os
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import cpu_backend
+    from bolt_amd.mi355x import _ops
+    be = _ops.backend_for(gpu_ctx.device)
+    vb = 16
+    per = vb // es
+    # [s, len, a, m] in 16-B vectors; group 3: run 0 -> [0,8) [10,18) [20,28),
+    # run 1 -> [30,36) [37,43) [44,50), run 2 -> [52,62) [62,72) [72,82) of 90
+    table = np.array([[0, 8, 0, 10], [12, 6, 30, 7], [30, 10, 52, 10]], np.int64)
+    group, nrec = 3, 12
+    src_rec, gstride = 40 * per, 90 * per
+    rng = np.random.default_rng(es)
+    src = rng.integers(0, 256, nrec * src_rec * es, dtype=np.uint8)
+    dst0 = rng.integers(0, 256, nrec // group * gstride * es, dtype=np.uint8)
+    g_src = torch.from_numpy(src).to(gpu_ctx.device)
+    g_dst = torch.from_numpy(dst0.copy()).to(gpu_ctx.device)
+    key = ("test_untiled", es)
+    be.record_runs(g_src, 0, g_dst, 0, nrec, src_rec, group, gstride, (table, vb), key, es)
+    assert be._maps[(g_src.device, key)][3] == 0  # the untiled kernel ran
+    want = torch.from_numpy(dst0.copy())
+    cpu_backend.CpuBackend().record_runs(torch.from_numpy(src.copy()), 0, want, 0, nrec, src_rec, group, gstride,
+                                         (table, vb), key, es)
+    assert torch.equal(g_dst.cpu(), want)
+    assert not np.array_equal(want.numpy(), dst0)  # the runs moved bytes
+
+
+@pytest.mark.gpu
+def test_record_runs_wrong_tiled_flag_stays_in_bounds(gpu_ctx):
+    """BM_RUNS_TILED on runs that do NOT tile the records (the flag is the
+    caller's claim; the library cannot see the device table): the destination
+    walk clamps every read into a run of a source record of its group, so the
+    call completes -- wrong bytes, no access outside the buffers (the source
+    sits between two guard regions that must stay unread-through: the result
+    holds only bytes of the source proper)."""
+    import ctypes
+    import torch
+    from bolt_amd.mi355x import _lib
+    lib = _lib.load()
+    es, vb = 8, 16
+    table = np.array([[0, 8, 0, 10], [12, 6, 30, 7], [30, 10, 52, 10]], np.int64)  # not a tiling
+    group, nrec = 3, 12
+    src_rec, gstride = 40 * 2, 90 * 2
+    n_src = nrec * src_rec
+    guard = 4096
+    buf = torch.full((guard + n_src + guard,), -1, dtype=torch.int64, device=gpu_ctx.device)
+    buf[guard:guard + n_src] = torch.arange(n_src, dtype=torch.int64, device=gpu_ctx.device)
+    src = buf[guard:guard + n_src]
+    dst = torch.full((nrec // group * gstride,), -2, dtype=torch.int64, device=gpu_ctx.device)
+    t = torch.from_numpy(table.reshape(-1).copy()).to(gpu_ctx.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(gpu_ctx.device).cuda_stream)
+    rc = lib.bm_record_runs(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), nrec, src_rec, group,
+                            gstride, 3, ctypes.c_void_p(t.data_ptr()), vb, _lib.RUNS_TILED, es, stream)
+    assert rc == 0
+    torch.cuda.synchronize(gpu_ctx.device)
+    out = dst.cpu().numpy()
+    assert out.min() >= 0 and out.max() < n_src  # every element came from the source proper

@@ -218,3 +218,25 @@ def test_context_opens_its_communicator_through_the_store():
     env = dict(os.environ, BM_ROOT=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), BM_PORT=str(port))
     r = subprocess.run([sys.executable, "-c", _CHILD], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("window_kb,total_kb", [(64, 1000), (32 << 10, 80 << 10)])
+def test_windowed_egress_over_rccl(comm, monkeypatch, window_kb, total_kb):
+    """dist.gather_windows -- the windowed egress toarray() / records() take
+    across GPUs -- with the RCCL all-gather (bm_allgatherv on a world-1
+    communicator) and the staged D2H, small windows (many all-gathers, no
+    staging) and 32-MiB windows (staged through the two page-locked buffers,
+    allocated once): the host bytes equal the device bytes."""
+    import torch
+    monkeypatch.setattr(D, "EGRESS_WINDOW", window_kb << 10)
+    ctx = _Ctx(comm)
+    n = total_kb << 10
+    x = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    calls = []
+
+    def gather(c, piece, part):
+        calls.append(sum(part))
+        return D._rccl_all_gather(c, piece, part)
+    out = D.gather_windows(ctx, x, [n], np.empty(n, np.uint8), gather)
+    assert np.array_equal(out, x.cpu().numpy())
+    assert len(calls) == -(-n // (window_kb << 10)) and max(calls) <= window_kb << 10
