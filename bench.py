@@ -742,8 +742,11 @@ def _short_kernel(name):
 
 
 def kernel_class(name):
-    """'marker' (torch's spin kernel), 'rccl', 'lib' (libbolt_mi355x), 'blit'
-    (the HIP runtime's copy kernels: hipMemcpyAsync on a shader) or 'other'."""
+    """'marker' (torch's spin kernel), 'rccl' (RCCL's device kernels,
+    ncclDevKernel_* / ncclKernel_*), 'lib' (libbolt_mi355x), 'blit' (the HIP
+    runtime's copy / fill kernels: hipMemcpyAsync on a shader), 'torch' (at::)
+    or 'other' (counted with RCCL's time: within a swap call nothing else
+    launches kernels)."""
     import re
     n = _short_kernel(name)
     if "spin_kernel" in n:
@@ -754,6 +757,8 @@ def kernel_class(name):
         return "lib"
     if "rocclr" in n or "__amd" in n:
         return "blit"
+    if n.startswith("at::") or "at::native" in n or "at::cuda" in n:
+        return "torch"
     return "other"
 
 
@@ -810,8 +815,8 @@ def rocprof_windows(trace_csv, marks, info, world):
         a = acc.setdefault(label, {"n": 0, "span": 0.0, "rccl": 0.0, "rccl_n": 0, "lib": 0.0, "blit": 0.0})
         a["n"] += 1
         a["span"] += (w1 - w0) / 1e6
-        a["rccl"] += _union_ms([(s, e) for s, e, c in ks if c == "rccl"])
-        a["rccl_n"] += sum(1 for _, _, c in ks if c == "rccl")
+        a["rccl"] += _union_ms([(s, e) for s, e, c in ks if c in ("rccl", "other")])
+        a["rccl_n"] += sum(1 for _, _, c in ks if c in ("rccl", "other"))
         a["lib"] += sum(e - s for s, e, c in ks if c == "lib") / 1e6
         a["blit"] += sum(e - s for s, e, c in ks if c == "blit") / 1e6
     out = {}

@@ -74,6 +74,58 @@ __device__ __forceinline__ void decomp2(uint64_t idx, const Decomp &d, int64_t &
   }
 }
 
+// decomp2 with the dim count known at compile time (ND >= 1): the loop
+// unrolls, so every divisor and stride is loaded into scalar registers once
+// per wave instead of once per dim per work item (the runtime loop indexes
+// the kernel-argument arrays with a loop counter, and each iteration waits
+// for its scalar loads).  ND = 0: the runtime loop.
+template <int ND>
+__device__ __forceinline__ void decomp_n(uint64_t idx, const Decomp &d, int64_t &so, int64_t &dof) {
+  if constexpr (ND == 0) {
+    decomp2(idx, d, so, dof);
+  } else {
+    so = 0;
+    dof = 0;
+#pragma unroll
+    for (int k = 0; k + 1 < ND; ++k) {
+      const uint64_t q = fd_div(idx, d.div[k]);
+      const uint64_t r = idx - q * d.div[k].d;
+      so += (int64_t)r * d.ss[k];
+      dof += (int64_t)r * d.ds[k];
+      idx = q;
+    }
+    so += (int64_t)idx * d.ss[ND - 1];
+    dof += (int64_t)idx * d.ds[ND - 1];
+  }
+}
+
+// decomp2 for up to 4 dims with every divisor and stride read at a constant
+// kernel-argument offset (an unrolled, predicated loop: the scalar loads are
+// hoisted to the kernel's start instead of one dependent load + wait per dim
+// and call); more dims take decomp2.  For kernels that decompose once per tile.
+__device__ __forceinline__ void decomp_le4(uint64_t idx, const Decomp &d, int64_t &so, int64_t &dof) {
+  const int n = d.n;
+  if (n > 4) {
+    decomp2(idx, d, so, dof);
+    return;
+  }
+  so = 0;
+  dof = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < n) {
+      uint64_t q = 0, r = idx;
+      if (k + 1 < n) {
+        q = fd_div(idx, d.div[k]);
+        r = idx - q * d.div[k].d;
+      }
+      so += (int64_t)r * d.ss[k];
+      dof += (int64_t)r * d.ds[k];
+      idx = q;
+    }
+  }
+}
+
 // Byte vectors for wide global accesses.
 template <int NB> struct VecB;
 template <> struct VecB<1> { typedef uint8_t t; };

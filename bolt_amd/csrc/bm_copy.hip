@@ -96,10 +96,15 @@ __device__ __forceinline__ uint64_t diag16_row(uint64_t row, const Diag16 &t) {
   return outer * t.grp.d + g * t.nc + c;
 }
 
-template <int VB>
+// One VB-byte vector per lane: vector v of row `row` (rows in destination
+// order, through the diagonal tiles when dg.on).  ND: the outer dims, known
+// at compile time for 1..kRcMaxND (0: a runtime loop); d's strides are in
+// BYTES; vpr_lg >= 0: vectors per row is 2^vpr_lg (a shift, not a division).
+constexpr int kRcMaxND = 6;
+template <int VB, int ND>
 __global__ void __launch_bounds__(kRcThreads)
     k_rowcopy(const char *__restrict__ src, char *__restrict__ dst, Decomp d,
-              FastDiv vpr, uint64_t total, int es, Diag16 dg) {
+              FastDiv vpr, int vpr_lg, uint64_t total, Diag16 dg) {
   typedef typename VecB<VB>::t V;
   const uint64_t step = (uint64_t)gridDim.x * kRcThreads * kUnroll;
   for (uint64_t base = (uint64_t)blockIdx.x * kRcThreads * kUnroll + threadIdx.x;
@@ -111,12 +116,12 @@ __global__ void __launch_bounds__(kRcThreads)
       const uint64_t g = base + (uint64_t)u * kRcThreads;
       doff[u] = -1;
       if (g < total) {
-        const uint64_t row = fd_div(g, vpr);
+        const uint64_t row = vpr_lg >= 0 ? g >> vpr_lg : fd_div(g, vpr);
         const uint64_t v = g - row * vpr.d;
         int64_t so, dof;
-        decomp2(dg.on ? diag16_row(row, dg) : row, d, so, dof);
-        reg[u] = __builtin_nontemporal_load(reinterpret_cast<const V *>(src + so * es + (int64_t)v * VB));
-        doff[u] = dof * es + (int64_t)v * VB;
+        decomp_n<ND>(dg.on ? diag16_row(row, dg) : row, d, so, dof);
+        reg[u] = __builtin_nontemporal_load(reinterpret_cast<const V *>(src + so + (int64_t)v * VB));
+        doff[u] = dof + (int64_t)v * VB;
       }
     }
 #pragma unroll
@@ -202,7 +207,7 @@ __global__ void __launch_bounds__(kThreads)
       ta = (ta - hi * d.asp.d) * d.aspq + hi;
     }
     int64_t so, dof;
-    decomp2(bt, d.batch, so, dof);
+    decomp_le4(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
 
     // load: lanes walk dim a (source-contiguous); all loads in flight first
@@ -293,7 +298,7 @@ __global__ void __launch_bounds__(NT)
     const uint64_t ta = fd_div(rem, d.ntB);
     uint64_t tb = rem - ta * d.ntB.d;
     int64_t so, dof;
-    decomp2(bt, d.batch, so, dof);
+    decomp_le4(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * TB;
 
     const T *s = src + so + a0 + b0 * d.sb;
@@ -385,7 +390,7 @@ __global__ void __launch_bounds__(NT)
     const uint64_t rem = t - bt * d.ntAB.d;
     const uint64_t ta = fd_div(rem, d.ntB);
     const uint64_t tb = rem - ta * d.ntB.d;
-    decomp2(bt, d.batch, so, dof);
+    decomp_le4(bt, d.batch, so, dof);
     a0 = (int64_t)ta * TA;
     b0 = (int64_t)tb * TB;
   };
@@ -492,7 +497,7 @@ __global__ void __launch_bounds__(kThreads)
     const uint64_t ta = fd_div(rem, d.ntB);
     uint64_t tb = rem - ta * d.ntB.d;
     int64_t so, dof;
-    decomp2(bt, d.batch, so, dof);
+    decomp_le4(bt, d.batch, so, dof);
     const int64_t a0 = (int64_t)ta * TA, b0 = (int64_t)tb * kRunTB;
     const int64_t na = min((int64_t)TA, d.La - a0);   // runs in this tile along A
     const int64_t nb = min((int64_t)kRunTB, d.Lb - b0);
@@ -572,6 +577,21 @@ int grid_for(uint64_t work_items, uint64_t per_block, uint64_t cap = 256ull * 16
 
 bool aligned(const void *p, int64_t a) { return ((uintptr_t)p % (uintptr_t)a) == 0; }
 
+template <int VB>
+void launch_rowcopy_nd(const char *src, char *dst, const Decomp &d, FastDiv fv, int vpr_lg, uint64_t total,
+                       const Diag16 &dg, int grid, hipStream_t st) {
+  switch (d.n) {
+    case 1: k_rowcopy<VB, 1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+    case 2: k_rowcopy<VB, 2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+    case 3: k_rowcopy<VB, 3><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+    case 4: k_rowcopy<VB, 4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+    case 5: k_rowcopy<VB, 5><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+    case 6: k_rowcopy<VB, 6><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+    default: k_rowcopy<VB, 0><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, vpr_lg, total, dg); break;
+  }
+  static_assert(kRcMaxND == 6, "launch_rowcopy_nd covers 1..kRcMaxND");
+}
+
 int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int es,
                    hipStream_t st) {
   const Dim inner = dims.back();
@@ -587,9 +607,13 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
     if (ok) break;
   }
   Decomp d;
-  if (!fill_decomp(d, outer)) {
-    bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)outer.size());
-    return BM_E_ARG;
+  {
+    std::vector<Dim> bytes(outer);  // the kernel's offsets are in bytes
+    for (Dim &x : bytes) { x.ss *= es; x.ds *= es; }
+    if (!fill_decomp(d, bytes)) {
+      bm_set_error("bm_copy_strided: too many dims after fusion (%d)", (int)outer.size());
+      return BM_E_ARG;
+    }
   }
   Diag16 dg{};
   {
@@ -619,17 +643,18 @@ int launch_rowcopy(const char *src, char *dst, const std::vector<Dim> &dims, int
   const uint64_t vpr = (uint64_t)(row_bytes / VB);
   const uint64_t total = rows * vpr;
   const FastDiv fv = make_fastdiv(vpr);
+  const int vpr_lg = (vpr & (vpr - 1)) == 0 ? __builtin_ctzll(vpr) : -1;
   const uint64_t per = (uint64_t)kRcThreads * kUnroll;
   const uint64_t need = (total + per - 1) / per;
   // one vector per lane (an XCD-grouped covering grid measured +5% in a C4
   // microbench but -3..-20% in the product A/B, profiles/r01_ab_rc)
   const int grid = need <= kRcGridCap ? (int)std::max<uint64_t>(need, 1) : grid_for(total, per, kRcGridCap);
   switch (VB) {
-    case 16: k_rowcopy<16><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
-    case 8: k_rowcopy<8><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
-    case 4: k_rowcopy<4><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
-    case 2: k_rowcopy<2><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
-    default: k_rowcopy<1><<<grid, kRcThreads, 0, st>>>(src, dst, d, fv, total, es, dg); break;
+    case 16: launch_rowcopy_nd<16>(src, dst, d, fv, vpr_lg, total, dg, grid, st); break;
+    case 8: launch_rowcopy_nd<8>(src, dst, d, fv, vpr_lg, total, dg, grid, st); break;
+    case 4: launch_rowcopy_nd<4>(src, dst, d, fv, vpr_lg, total, dg, grid, st); break;
+    case 2: launch_rowcopy_nd<2>(src, dst, d, fv, vpr_lg, total, dg, grid, st); break;
+    default: launch_rowcopy_nd<1>(src, dst, d, fv, vpr_lg, total, dg, grid, st); break;
   }
   return BM_OK;
 }

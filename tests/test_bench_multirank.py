@@ -353,6 +353,9 @@ def test_rocprof_windows_on_a_synthetic_trace():
     assert line["xgmi"]["pack_unpack_frac"] == 0.125 and line["rocprof"]["ops"] is w
     assert bench.kernel_class("void k_transpose<unsigned int, 64, 256, 4, 4, false>(X)") == "lib"
     assert bench.kernel_class("ncclDevKernel_Generic_4(x)") == "rccl"
+    assert bench.kernel_class("__amd_rocclr_copyBuffer") == "blit"
+    assert bench.kernel_class("at::cuda::(anonymous namespace)::spin_kernel(long)") == "marker"
+    assert bench.kernel_class("void at::native::vectorized_elementwise_kernel<16, X>(int, X)") == "torch"
 
 
 def test_rocprof_only_on_gpu_ranks(monkeypatch):
