@@ -192,7 +192,7 @@ def _every_op_checked(rec):
     assert all(o["ck"] == "exact" or o["ck"].startswith("ok ") for o in rec["ops"].values()), rec["ops"]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_bench_launches_its_ranks(world):
     """`bench.py --gpus N` without WORLD_SIZE starts the N rank processes itself
     and rank 0's JSON line comes back: n_gpus N, the C2 headline weak-scaled,
