@@ -99,6 +99,8 @@ def parse(argv=None):
                     help="skip the C1/C3/C4/C5 sub-records of the default (C2) run")
     ap.add_argument("--config-steps", type=int, default=3)
     ap.add_argument("--no-checks", action="store_true", help="skip the post-timing result checks")
+    ap.add_argument("--no-sweeps", action="store_true",
+                    help="N > 1: skip the all-to-all size sweep and the swap's pipeline-depth sweep")
     ap.add_argument("--detail", default=None,
                     help="file for the full record with its prose (default gpurun_out/bench_detail_n<N>.json)")
     # internal: rocprofv3 child, CPU-baseline child, rehearsal shapes (JSON {config: shape}: a weak
@@ -823,9 +825,12 @@ def rocprof_windows(trace_csv, marks, info, world):
     peak = (world - 1) * XGMI_LINK_GBPS
     for label, a in acc.items():
         n = a["n"]
-        o = {"n": n, "span": round(a["span"] / n, 4), "rccl": round(a["rccl"] / n, 4),
-             "rccl_n": round(a["rccl_n"] / float(n), 2), "lib": round(a["lib"] / n, 4),
-             "blit": round(a["blit"] / n, 4)}
+        o = {"n": n, "span": round(a["span"] / n, 3), "rccl": round(a["rccl"] / n, 3),
+             "lib": round(a["lib"] / n, 3)}
+        if a["rccl_n"]:
+            o["rccl_n"] = round(a["rccl_n"] / float(n), 1)
+        if a["blit"]:
+            o["blit"] = round(a["blit"] / n, 3)
         payload, local = (info or {}).get(label, (0, 0))
         if payload and o["rccl"] > 0:
             o["xgmi_GBs"] = round(payload / (o["rccl"] / 1e3) / 1e9, 1)
@@ -837,9 +842,9 @@ def rocprof_windows(trace_csv, marks, info, world):
 
 
 def merge_rocprof(line, ops, stats_file):
-    """rocprof_windows' numbers into the record: ``rocprof`` (every op), the
-    headline swap's RCCL time into ``xgmi`` and each config op's into its
-    record."""
+    """rocprof_windows' numbers into the record: ``rocprof`` (every op of
+    every config, keyed "cfg.op") and the headline swap's RCCL time into
+    ``xgmi``."""
     line["rocprof"] = {"rank": 0, "stats": stats_file, "ops": ops}
     head = "%s.%s" % (line.get("config", {}).get("name", "C2"), next(iter(line.get("ops", {"swap": 0}))))
     h = ops.get(head)
@@ -850,16 +855,6 @@ def merge_rocprof(line, ops, stats_file):
             line["xgmi"]["rocprof_frac"] = h["xgmi_frac"]
         if "pu_frac" in h:
             line["xgmi"]["pack_unpack_frac"] = h["pu_frac"]
-    for cfg, rec in line.get("configs", {}).items():
-        for op, o in rec.get("ops", {}).items():
-            r = ops.get("%s.%s" % (cfg, op))
-            if r:
-                o["k_ms"] = r["lib"]
-                if r["rccl"]:
-                    o["rccl_ms"] = r["rccl"]
-                for k in ("xgmi_frac", "pu_frac"):
-                    if k in r:
-                        o[k] = r[k]
 
 
 # ------------------------------------------------------------ CPU baseline --
@@ -1412,6 +1407,60 @@ def main():
         barrier()
         marks.append([cfg, [n for n, _, _ in ops], steps])
 
+    def call_ms(call, reps):
+        """Mean ms of ``reps`` calls between events on the current stream after
+        one warm-up call (a swap's events bracket its whole exchange: the last
+        unpack waits for the last all-to-all), max over ranks."""
+        r = call()
+        del r
+        barrier()
+        evs = []
+        for _ in range(reps):
+            e0, e1 = make_event(dev), make_event(dev)
+            e0.record()
+            r = call()
+            e1.record()
+            del r
+            evs.append((e0, e1))
+        barrier()
+        return max_over_ranks(float(np.mean([a.elapsed_time(z) for a, z in evs])))
+
+    def stage_sweep(swap_call, reps=3):
+        """The swap's exchange time at pipeline depths K = 1..16 (dist.STAGES):
+        tuning data for dist.STAGE_BYTES_BY_WORLD from the run itself."""
+        out = {}
+        try:
+            for k in (1, 2, 4, 8, 16):
+                bdist.STAGES = k
+                out[str(k)] = round(call_ms(swap_call, reps), 3)
+        finally:
+            bdist.STAGES = None
+        progress("swap exchange ms by pipeline depth: %s" % out)
+        return out
+
+    def a2a_sweep(reps=5):
+        """The xGMI all-to-all itself: bm_alltoallv (RCCL send / recv group) of
+        B bytes to every peer, no pack / unpack; per size [ms, GB/s each rank
+        sends, fraction of (G-1) x 153 GB/s]."""
+        out = {}
+        G = world
+        for mib in (4, 16, 64):
+            per = mib << 20
+            send = torch.empty(per * G, dtype=torch.uint8, device=dev)
+            sizes = [per] * G
+
+            def xchg():
+                recv, work = bdist.all_to_all_bytes(ctx, send, sizes, sizes, 8, async_op=True)
+                if work is not None:
+                    work.wait()
+                return recv
+            ms = call_ms(xchg, reps)
+            gbs = per * (G - 1) / (ms / 1e3) / 1e9
+            out["%dM" % mib] = [round(ms, 4), round(gbs, 1), round(gbs / ((G - 1) * XGMI_LINK_GBPS), 4)]
+            del send
+        progress("all-to-all per peer size -> [ms, GB/s, frac]: %s" % out)
+        return out
+
     def run_all_checks(cfg, b, gshape, dtype, rec_ops):
         """Checks of every op (run_checks) into rec_ops[name]["ck"]; returns all-ok (None: skipped)."""
         if args.no_checks:
@@ -1559,6 +1608,9 @@ def main():
             times = per_op_ms(ops, steps)
             line["ops"] = {name: op_rec(nb, *times[name]) for name, _, nb in ops}
         marked_pass(cfg, b, ops, steps)
+        if world > 1 and not args.no_sweeps:
+            line["xgmi"]["stages_ms"] = stage_sweep(ops[0][1])
+            line["a2a"] = a2a_sweep()
         ok = run_all_checks(cfg, b, gshape, dtype, line.setdefault("ops", {}))
         line["checks_ok"] = ok
         if world > 1:

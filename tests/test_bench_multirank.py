@@ -221,6 +221,9 @@ def test_bench_launches_its_ranks(world):
     assert d["configs"]["C4"]["ops"]["var"]["ck"].startswith("ok ")
     assert "target64" not in d  # the 64 GiB target is a one-GPU record
     assert "rocprof_marks" not in d and "rocprof" not in d  # no profiler on the CPU rehearsal
+    # tuning data of the N-rank run: the swap by pipeline depth, the bare all-to-all by size
+    assert set(d["xgmi"]["stages_ms"]) == {"1", "2", "4", "8", "16"}
+    assert set(d["a2a"]) == {"4M", "16M", "64M"} and all(len(v) == 3 and v[0] > 0 for v in d["a2a"].values())
 
 
 def test_bench_refuses_gpu_count_mismatch():
@@ -346,8 +349,7 @@ def test_rocprof_windows_on_a_synthetic_trace():
     assert m["span"] == 0.238 and m["rccl"] == 0.02 and m["lib"] == 0.2 and "xgmi_frac" not in m
     with pytest.raises(RuntimeError):
         bench.rocprof_windows(trace, [["C2", ["swap", "mean"], 3]], info, world=4)
-    line = {"config": {"name": "C2"}, "ops": {"swap": {}, "mean": {}}, "xgmi": {},
-            "configs": {"C3": {"ops": {"swap": {}}}}}
+    line = {"config": {"name": "C2"}, "ops": {"swap": {}, "mean": {}}, "xgmi": {}}
     bench.merge_rocprof(line, w, "gpurun_out/x.csv")
     assert line["xgmi"]["rocprof_ms"] == 0.5 and line["xgmi"]["rocprof_frac"] == s["xgmi_frac"]
     assert line["xgmi"]["pack_unpack_frac"] == 0.125 and line["rocprof"]["ops"] is w
