@@ -1276,6 +1276,9 @@ def main():
     if world > 1 and not rehearsal_knobs() and world > visible_gpus():
         sys.stderr.write("bench.py: WORLD_SIZE=%d but %d GPU(s) visible\n" % (world, visible_gpus()))
         return 2
+    # a stalled exchange ends the run with BoltCommError well inside any
+    # driver's limit (a legitimate exchange here takes milliseconds)
+    os.environ.setdefault("BOLT_AMD_COMM_TIMEOUT", "180")
     profiling = rocprof_wanted(args, world, where)
     if profiling and rank == 0 and not os.environ.get(PROFILED_ENV):
         return rocprof_rank0(sys.argv[1:], world)
