@@ -106,9 +106,18 @@ def raw_stream(device):
     """Handle of torch's current HIP stream on ``device`` (what
     ``torch.cuda.current_stream(device).cuda_stream`` returns, without building
     a Stream object: ~2 us less per launch, profiles/r01_host_breakdown.log)."""
-    import torch
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    return torch._C._cuda_getCurrentRawStream(idx)
+    global _raw_stream_of
+    if _raw_stream_of is None:
+        import torch
+        _raw_stream_of = torch._C._cuda_getCurrentRawStream
+    idx = device.index
+    if idx is None:
+        import torch
+        idx = torch.cuda.current_device()
+    return _raw_stream_of(idx)
+
+
+_raw_stream_of = None  # torch._C._cuda_getCurrentRawStream, bound on first use
 
 
 class HipBackend(object):
@@ -124,13 +133,15 @@ class HipBackend(object):
         self._args = {}  # (shape, perm) -> ctypes arguments of bm_permute
         self._ws = {}    # reduction -> workspace bytes
 
+    # Pointer and stream arguments go to ctypes as plain ints (the argtypes
+    # are c_void_p): no c_void_p object per argument on the launch path.
     @staticmethod
     def _stream(t):
-        return ctypes.c_void_p(raw_stream(t.device))
+        return raw_stream(t.device)
 
     @staticmethod
     def _ptr(t, off=0):
-        return ctypes.c_void_p(t.data_ptr() + int(off))
+        return t.data_ptr() + int(off)
 
     def host_writable(self, t):
         """True if kernels can store into host tensor ``t`` at its own address."""
@@ -157,8 +168,10 @@ class HipBackend(object):
             if len(self._args) > 4096:
                 self._args.clear()
             self._args[key] = args
-        _lib.check(self.lib.bm_permute(self._ptr(src), self._ptr(dst), args[0], args[1], args[2], int(es),
-                                       self._stream(src)), "bm_permute")
+        rc = self.lib.bm_permute(src.data_ptr(), dst.data_ptr(), args[0], args[1], args[2], es,
+                                 raw_stream(src.device))
+        if rc:
+            _lib.check(rc, "bm_permute")
 
     def gather_rows(self, src, src_off, dst, dst_off, n_outer, src_rows, row_bytes, idx):
         """dst[a, j, :] = src[a, idx[j], :] (byte offsets; idx a host int64 array, bounds-checked)."""
@@ -286,9 +299,10 @@ class HipBackend(object):
 
     def reduce(self, stat, src, code, O, R, I, out, out_code):
         ws, nws = self._workspace(stat, code, O, R, I, src.device)
-        _lib.check(self.lib.bm_reduce(stat, self._ptr(src), code, O, R, I, self._ptr(out), out_code,
-                                      self._ptr(ws) if ws is not None else None, nws,
-                                      self._stream(src)), "bm_reduce")
+        rc = self.lib.bm_reduce(stat, src.data_ptr(), code, O, R, I, out.data_ptr(), out_code,
+                                ws.data_ptr() if ws is not None else None, nws, raw_stream(src.device))
+        if rc:
+            _lib.check(rc, "bm_reduce")
 
     def state_bytes(self, stat, code, nout):
         n = ctypes.c_size_t(0)

@@ -95,9 +95,19 @@ def _check_swap_plan(vshape, dtype, size):
         raise type(err)(*err.args)
 
 
-_SWAP_PLANS = {}   # (shape, split, dtype, kaxes, vaxes, size) -> (perm, newsplit) | _NOOP
+_SWAP_PLANS = {}   # (shape, split, dtype, kaxes, vaxes, size) -> _move_plan | _NOOP
 _NOOP = object()
+
+
+def _move_plan(shape, perm, split):
+    """What x.transpose(perm) with the given split needs, from the shape alone:
+    (perm, split, new shape, identity, only unit axes move)."""
+    perm = tuple(int(p) for p in perm)
+    moved = [p for p in perm if shape[p] != 1]
+    return (perm, int(split), tuple(shape[p] for p in perm), perm == tuple(range(len(shape))),
+            moved == sorted(moved))
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
+_STAT_AXES = {}  # (shape, axis as given) -> (validated axis tuple, records after _align)
 
 
 class BoltArrayMI355X(BoltArray):
@@ -214,6 +224,14 @@ class BoltArrayMI355X(BoltArray):
         return BoltArrayMI355X(data, shape=shape, split=split, dtype=self._dtype if dtype is None else dtype,
                                context=self._ctx, npartitions=self._npartitions)
 
+    def _derive(self, data, shape, split):
+        """_like for a ``shape`` that is already a tuple of ints and the same
+        dtype: the constructor's coercions skipped (the swap's launch path)."""
+        new = object.__new__(BoltArrayMI355X)
+        new.__dict__.update(_data=data, _shape=shape, _split=split, _dtype=self._dtype, _mode='mi355x',
+                            _ordered=True, _ctx=self._ctx, _npartitions=self._npartitions)
+        return new
+
     @property
     def _backend(self):
         return backend_for(self._data.device)
@@ -277,18 +295,20 @@ class BoltArrayMI355X(BoltArray):
     # ------------------------------------------------------------ movement
     def _permute(self, perm, split):
         """x.transpose(perm) as a new array with the given split (one kernel / one all-to-all)."""
-        perm = [int(p) for p in perm]
-        new_shape = tuple(self._shape[p] for p in perm)
-        if perm == list(range(self.ndim)):
-            return self._like(self._data, new_shape, split)
-        moved = [p for p in perm if self._shape[p] != 1]
-        if moved == sorted(moved) and (self._ctx.world_size == 1 or perm[0] == 0):
-            # only unit axes move: the C-order bytes are already the result's
-            # (across GPUs the leading axis, hence every slab, stays put)
-            return self._like(self._data, new_shape, split)
-        data = permute_sharded(self._ctx, self._backend, self._data, self._shape, perm,
-                               self._dtype.itemsize)
-        return self._like(data, new_shape, split)
+        return self._move(_move_plan(self._shape, perm, split))
+
+    def _move(self, mv):
+        """Run a _move_plan on this array."""
+        perm, split, new_shape, relabel, units_only = mv
+        if relabel or (units_only and (perm[0] == 0 or self._ctx.world_size == 1)):
+            # no bytes move: the identity, or only unit axes move, so the C-order
+            # bytes are already the result's (across GPUs the leading axis,
+            # hence every slab, stays put)
+            data = self._data
+        else:
+            data = permute_sharded(self._ctx, backend_for(self._data.device), self._data, self._shape, perm,
+                                   self._dtype.itemsize)
+        return self._derive(data, new_shape, split)
 
     def chunk(self, size="150", axis=None, padding=None):
         """Chunk the values of every record (array.py:678-714) -> ChunkedArrayMI355X."""
@@ -308,25 +328,32 @@ class BoltArrayMI355X(BoltArray):
         chunking; it is validated the same way (getplan + _chunk checks) and
         does not change the result.  Executed as one permute kernel.
         """
-        try:  # host plan of an already validated (shape, split, dtype, axes, size)
-            key = (self._shape, self._split, self._dtype, tuple(int(k) for k in tupleize(kaxes)),
-                   tuple(int(v) for v in tupleize(vaxes)), size if type(size) is str else tupleize(size))
-            hash(key)
-        except (TypeError, ValueError):
-            key = None
-        hit = _SWAP_PLANS.get(key) if key is not None else None
-        if hit is not None:
-            if hit is _NOOP:
-                return self
-            return self._permute(*hit)
-        plan = self._swap_plan(kaxes, vaxes, size)
-        if key is not None:
+        # host plan of an already validated (shape, split, dtype, axes, size):
+        # first under the arguments as given, then canonicalised
+        try:
+            raw = (self._shape, self._split, self._dtype, kaxes, vaxes, size)
+            hit = _SWAP_PLANS.get(raw)
+        except TypeError:  # unhashable arguments (lists)
+            raw = hit = None
+        if hit is None:
+            try:
+                key = (self._shape, self._split, self._dtype, tuple(int(k) for k in tupleize(kaxes)),
+                       tuple(int(v) for v in tupleize(vaxes)), size if type(size) is str else tupleize(size))
+                hash(key)
+            except (TypeError, ValueError):
+                key = None
+            hit = _SWAP_PLANS.get(key) if key is not None else None
+            if hit is None:
+                plan = self._swap_plan(kaxes, vaxes, size)
+                hit = _NOOP if plan is None else _move_plan(self._shape, *plan)
             if len(_SWAP_PLANS) > 4096:
                 _SWAP_PLANS.clear()
-            _SWAP_PLANS[key] = _NOOP if plan is None else plan
-        if plan is None:
+            for k in (key, raw):
+                if k is not None:
+                    _SWAP_PLANS[k] = hit
+        if hit is _NOOP:
             return self
-        return self._permute(*plan)
+        return self._move(hit)
 
     def _swap_plan(self, kaxes, vaxes, size):
         """Validation and net permutation of swap: (perm, newsplit), or None for a no-op."""
@@ -791,16 +818,22 @@ class BoltArrayMI355X(BoltArray):
 
     def _stat(self, axis=None, func=None, name=None, keepdims=False):
         """Statistic over ``axis`` (array.py:284-334); results are host arrays / scalars."""
-        if axis is None:
-            axis = list(range(len(self.shape)))
-        axis = tupleize(axis)
-
-        if func and not name:
-            return self.reduce(func, axis, keepdims)
-
         if name and not func:
-            inshape(self.shape, axis)
-            if self._nrecords(axis) == 0:
+            try:  # axes already validated for this shape, keyed by the argument as given
+                ak = (self._shape, axis)
+                hit = _STAT_AXES.get(ak)
+            except TypeError:  # unhashable axis (a list)
+                ak = hit = None
+            if hit is None:
+                ax = tupleize(list(range(len(self.shape))) if axis is None else axis)
+                inshape(self.shape, ax)
+                hit = (ax, self._nrecords(ax))
+                if ak is not None:
+                    if len(_STAT_AXES) > 4096:
+                        _STAT_AXES.clear()
+                    _STAT_AXES[ak] = hit
+            axis, nrec = hit
+            if nrec == 0:
                 # no records after _align: the merged StatCounter is the empty one
                 # (statcounter.py:28-41, :109-130): mean 0.0, variance / stdev nan
                 arr = 0.0 if name == 'mean' else float('nan')
@@ -812,6 +845,12 @@ class BoltArrayMI355X(BoltArray):
                 for i in axis:
                     arr = np.expand_dims(arr, axis=i)
             return BoltArrayLocal(arr).toscalar()
+
+        if axis is None:
+            axis = list(range(len(self.shape)))
+        axis = tupleize(axis)
+        if func and not name:
+            return self.reduce(func, axis, keepdims)
 
         raise ValueError('Must specify either a function or a statistic name.')
 
