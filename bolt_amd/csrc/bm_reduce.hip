@@ -58,6 +58,9 @@ constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane 
 #ifndef BM_RED_XCD
 #define BM_RED_XCD 1  // rows kernel: blocks dealt to one XCD take consecutive rows (C2 mean / std +3-4%, profiles/r02_ab_redxcd.log)
 #endif
+#ifndef BM_COLS_XCD
+#define BM_COLS_XCD 1  // column kernels: blocks dealt to one XCD take consecutive column tiles (C4 var +1.1%, 64 GiB-target-shaped mean / std over axis 0 +2.2% / +1.6%, profiles/r05h_ab_cols_xcd.log)
+#endif
 
 enum Mode {
   M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4, M_MAX = 5, M_MIN = 6,
@@ -417,6 +420,18 @@ __device__ __forceinline__ void emit(const Sink &sk, int64_t e, double n, double
 }
 
 // ------------------------------------------------------------------ cols --
+// blockIdx.x, with the blocks the hardware deals to one XCD (every 8th)
+// remapped to consecutive indices when BM_COLS_XCD (a bijection of the grid):
+// each XCD then reads one contiguous range of every row
+__device__ __forceinline__ uint64_t xcd_block() {
+  uint64_t bid = blockIdx.x;
+  if (BM_COLS_XCD) {
+    const uint64_t g8 = gridDim.x / 8 * 8;
+    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
+  }
+  return bid;
+}
+
 struct ColsDesc {
   int64_t O, R, I;
   int64_t rchunk;
@@ -437,7 +452,7 @@ __global__ void __launch_bounds__(kThreads)
   double *sm0 = smem;
   double *sm1 = smem + kThreads * VEC;
   double *smn = smem + 2 * kThreads * VEC;
-  const uint64_t ot = (uint64_t)d.tile0 + blockIdx.x;
+  const uint64_t ot = (uint64_t)d.tile0 + xcd_block();
   const uint64_t o = fd_div(ot, d.ntc);
   const uint64_t tc = ot - o * d.ntc.d;
   const int64_t c = blockIdx.y;
@@ -845,7 +860,7 @@ __global__ void __launch_bounds__(kThreads)
   extern __shared__ double smem[];
   uint64_t *l1 = reinterpret_cast<uint64_t *>(smem);
   uint64_t *l2 = l1 + kThreads * VEC;
-  const uint64_t ot = (uint64_t)d.tile0 + blockIdx.x;
+  const uint64_t ot = (uint64_t)d.tile0 + xcd_block();
   const uint64_t o = fd_div(ot, d.ntc);
   const uint64_t tc = ot - o * d.ntc.d;
   const int64_t c = blockIdx.y;
