@@ -110,6 +110,10 @@ class ChunkedArrayMI355X(object):
         # records carry no chunk id (chunk.py:335-345); chunk() of an all-key
         # array appends one with chunk id 0 (chunk.py:113-118)
         self._bare_singleton = False
+        # keys_to_values of an array whose values are (1,) squeezes each new
+        # record (chunk.py:284-287: squeeze drops EVERY unit axis, so a moved
+        # key of extent 1 leaves 0-d records); records() shows them that way
+        self._squeezed_records = False
 
     # ---------------------------------------------------------- properties
     @property
@@ -344,8 +348,10 @@ class ChunkedArrayMI355X(object):
             newshape = newshape[:-1]
             newplan = newplan[:-1]
             newpadding = newpadding[:len(newplan)]
-            return self._rechunk(dense, perm[:-1], self._shape[:-1], newshape, newsplit,
-                                 newplan, newpadding)
+            res = self._rechunk(dense, perm[:-1], self._shape[:-1], newshape, newsplit,
+                                newplan, newpadding)
+            res._squeezed_records = True
+            return res
         return self._rechunk(dense, perm, self._shape, newshape, newsplit, newplan, newpadding)
 
     def values_to_keys(self, axes):
@@ -547,8 +553,8 @@ class ChunkedArrayMI355X(object):
                 cs = g.chunk_shape(j)
                 n = int(np.prod(cs, dtype=np.int64))
                 chk = () if self._bare_singleton else tuple(int(c) for c in j)
-                yield (tuple(int(k) for k in key) + chk,
-                       host[base + off: base + off + n].reshape(cs).copy())
+                v = host[base + off: base + off + n].reshape(cs).copy()
+                yield (tuple(int(k) for k in key) + chk, v.squeeze() if self._squeezed_records else v)
 
     def tordd(self):
         from bolt_amd.mi355x.records import RecordView

@@ -339,6 +339,12 @@ def gen_moves():
         (spec((2, 2, 5, 6)), (0, 1), (2, 2), 1, [("v2k", (0,), None)]),
         (spec((3, 4, 9, 10), "float64", "normal", 11), (0, 1), (4, 4), (1, 2), [("k2v", (0,), None), ("v2k", (1,), None)]),
         (spec((3, 4, 9, 10), "float64", "normal", 11), (0, 1), (4, 4), 2, [("v2k", (0, 1), None), ("k2v", (1, 2), (2, 3))]),
+        # a moved key of extent 1 when the values are (1,): keys_to_values
+        # squeezes the old (1,) and the values are (1,) again, so unchunk
+        # squeezes once more (chunk.py:284-287, :193-197)
+        (spec((4, 1, 3, 2, 1)), (0, 1, 2, 3), (1,), None, [("k2v", (1,), None)]),
+        (spec((4, 1, 3, 1)), (0, 1, 2), (1,), None, [("k2v", (1,), None)]),
+        (spec((4, 1, 3, 2)), (0, 1, 2), (2,), None, [("k2v", (1,), None)]),
     ]
     for s, axis, size, pad, steps in items:
         x = make_input(s)

@@ -10,6 +10,8 @@ rowcopy, record-map gathers with parts, row and column reductions).
 Data movement must be bit-exact; statistics use the bar of
 tests/test_golden_api.py (rtol 1e-6 float32 / 1e-12 float64, scaled).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -18,6 +20,8 @@ from oracle import bolt_oracle as O
 
 DTYPES = [np.float32, np.float64, np.uint8, np.int16, np.uint16, np.int32]
 NCASES = 200
+# a soak run takes other seeds: BOLT_AMD_FUZZ_SEEDS=start:stop (default 0:NCASES)
+_SEEDS = range(*[int(v) for v in os.environ.get("BOLT_AMD_FUZZ_SEEDS", "0:%d" % NCASES).split(":")])
 
 
 def _case(seed):
@@ -48,7 +52,7 @@ def _records_equal(got, want):
         assert _exact(gv, np.ascontiguousarray(wv)), gk
 
 
-@pytest.mark.parametrize("seed", range(NCASES))
+@pytest.mark.parametrize("seed", _SEEDS)
 def test_fuzz_against_oracle(bctx, seed):
     check_case(bctx, seed)
 

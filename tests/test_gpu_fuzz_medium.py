@@ -8,6 +8,8 @@ spark/array.py:716-833, chunk.py:202-347); the record-level oracle covers the
 same operations at small sizes (tests/test_fuzz_oracle.py).  Statistics are
 checked against a longdouble computation with the bar of test_fuzz_oracle.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -33,7 +35,11 @@ def _exact(a, b):
     return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
 
 
-@pytest.mark.parametrize("seed", range(240))
+# a soak run takes other seeds: BOLT_AMD_FUZZ_SEEDS=start:stop (default 0:240)
+_SEEDS = range(*[int(v) for v in os.environ.get("BOLT_AMD_FUZZ_SEEDS", "0:240").split(":")])
+
+
+@pytest.mark.parametrize("seed", _SEEDS)
 def test_medium_fuzz(gpu_ctx, seed):
     gctx = gpu_ctx
     rng = np.random.default_rng(5000 + seed)
@@ -74,6 +80,11 @@ def test_medium_fuzz(gpu_ctx, seed):
     want = x.transpose(order)
     if vshape == (1,):
         want = want.reshape(want.shape[:-1])  # the all-keys singleton is squeezed (chunk.py:284-287)
+        if want.shape[split - 1:] == (1,):
+            # a moved key of extent 1 leaves the values (1,) again: unchunk
+            # squeezes once more (chunk.py:193-197; the reference itself gives
+            # (4, 1, 3, 2, 1) split 4 -> k2v((1,)) -> unchunk -> (4, 3, 2))
+            want = want.reshape(want.shape[:-1])
     assert _exact(c.keys_to_values((k,)).unchunk().toarray(), want), k
     if ndim - split > 1:
         v = int(rng.integers(0, ndim - split))
