@@ -626,7 +626,7 @@ class BoltArrayMI355X(BoltArray):
         index returns a scalar.
         """
         from bolt_amd.mi355x import indexing
-        index, int_locs, kind = indexing.normalize(index, self._shape)
+        index, int_locs, kind = indexing.normalize(index, self._shape, self._split)
         es = self._dtype.itemsize
         if kind == 'basic':
             starts = [s.start for s in index]

@@ -471,6 +471,11 @@ def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es):
     """
     shape = tuple(int(x) for x in shape)
     out_shape = tuple(int(x) for x in out_shape)
+    for d, n, s0, st in zip(shape, out_shape, starts, steps):
+        # every selected index inside its axis: the copies below read through
+        # raw device pointers
+        if n > 0 and not (0 <= s0 < d and 0 <= s0 + (n - 1) * st < d):
+            raise ValueError("selection %d::%d of %d elements leaves an axis of %d" % (s0, st, n, d))
     in_b = ctx.bounds(shape[0])
     out_b = ctx.bounds(out_shape[0])
     r = ctx.rank

@@ -27,12 +27,12 @@ import numpy as np
 from bolt_amd.mi355x.dist import all_to_all_bytes, _empty, _unit
 
 
-def normalize(index, shape):
+def normalize(index, shape, split):
     """The reference's index normalisation and bounds checks (array.py:629-659).
 
     Returns (index list, int_locs, kind) with slices slicified and list
     indices as ndarrays (negatives wrapped); kind is 'basic' / 'advanced' /
-    'mixed'.
+    'mixed'.  Every returned slice selects indices inside its axis (below).
     """
     from bolt_amd.utils import slicify
     if isinstance(index, tuple):
@@ -57,6 +57,8 @@ def normalize(index, shape):
             if minval > size - 1 or maxval < 1 or minval >= maxval:
                 raise ValueError("Index {} in dimension {} with shape {} would "
                                  "produce an empty dimension".format(idx, n, size))
+            if slc.step < 0 and slc.start == size:
+                slc = _past_end(idx, n, size, slc, n < split)
             index[n] = slc
         else:
             adjusted = np.asarray(idx)
@@ -79,6 +81,23 @@ def normalize(index, shape):
                                   "with advanced indexing (lists, tuples, and ndarrays), "
                                   "can only have a single advanced index")
     return index, int_locs, kind
+
+
+def _past_end(idx, n, size, slc, on_key):
+    """A negative-step slice that slicify leaves starting AT the end (it clamps
+    only start > dim, bolt/utils.py:136).  The reference's shape counts that
+    phantom element (array.py:510).  On a key axis no record carries it, so the
+    records fall short of the shape and the array cannot be collected: refused.
+    On a value axis numpy slices each record (array.py:505-506) from dim - 1:
+    the array is numpy's selection when the two counts agree, uncollectable
+    otherwise (refused).  Returns the equivalent in-bounds slice."""
+    stop = None if slc.stop == -1 else slc.stop
+    declared = int(np.ceil((slc.stop - slc.start) / float(slc.step)))
+    if not on_key and len(range(size)[slice(slc.start, stop, slc.step)]) == declared:
+        return slice(size - 1, slc.stop, slc.step)
+    raise ValueError("Index {} in dimension {} with shape {} starts past the end with a negative "
+                     "step: the reference's array would hold fewer elements than its shape"
+                     .format(idx, n, size))
 
 
 def _listify(lst, dim):
