@@ -182,8 +182,9 @@ def test_api_fuzz(bctx, seed):
     thr = float(np.median(x))
     srt = bool(rng.random() < 0.5)
 
-    def keep_rec(v):
-        return float(np.asarray(v, dtype=np.float64).sum()) > thr * max(1, np.asarray(v).size)
+    def keep_rec(v):  # a numpy record (the oracle) or a device tensor (bolt_amd on a GPU)
+        tot = v.double().sum() if hasattr(v, "double") else v.astype(np.float64).sum()
+        return float(tot) > thr * max(1, v.reshape(-1).shape[0])
     want, got = _raises_like(lambda: O.filter_(rs, keep_rec, axis=fax, sort=srt),
                              lambda: b.filter(keep_rec, axis=fax, sort=srt))
     if want is not None:
