@@ -1,5 +1,8 @@
-"""CPU soak of the seeded fuzz suites on several ranks over gloo, with the
-numpy test executor: every rank runs the same seeded case on a context that
+"""Soak of the seeded fuzz suites on several ranks over gloo -- on the CPU
+with the numpy test executor, or (device cuda:0) every rank on the one GPU
+with the HIP kernels and the exchanges staged through the host (the
+rehearsal executor: RCCL refuses two ranks on one GPU).  Every rank runs the
+same seeded case on a context that
 spans the ranks, so arrays are sharded (ragged and empty slabs) and every
 exchange path runs -- swaps, sharded statistics, chunk moves (suite
 "oracle", tests/test_fuzz_oracle.py), indexing and its row exchanges
@@ -8,6 +11,7 @@ reductions / map / filter / stacks ("api", tests/test_api_fuzz.py) -- each
 compared with the oracle.
 
     python tools/dist_fuzz_soak.py oracle:2:200:700 getitem:3:0:2000 api:4:0:1000
+    BOLT_AMD_SOAK_DEVICE=cuda:0 python tools/dist_fuzz_soak.py getitem:2:0:500
 """
 import os
 import sys
@@ -40,8 +44,12 @@ def _worker(rank, world, port, errq, suite, seeds):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from bolt_amd import MI355XContext
         import cpu_backend
-        cpu_backend.install()
-        ctx = MI355XContext(device="cpu")
+        device = os.environ.get("BOLT_AMD_SOAK_DEVICE", "cpu")
+        if device == "cpu":
+            cpu_backend.install()
+        else:
+            cpu_backend.install_host_staged_gpu()
+        ctx = MI355XContext(device=device)
         case = _case_fn(suite)
         ran = skipped = 0
         for seed in seeds:
@@ -54,7 +62,9 @@ def _worker(rank, world, port, errq, suite, seeds):
                     continue
                 raise AssertionError("%s seed %d failed: %s" % (suite, seed, traceback.format_exc()[-2500:]))
         if rank == 0:
-            print("  rank 0: %d cases compared, %d skipped" % (ran, skipped), flush=True)
+            print("  rank 0 on %s (%s): %d cases compared, %d skipped"
+                  % (ctx.device, type(ctx.backend).__name__ if hasattr(ctx, "backend") else "-", ran, skipped),
+                  flush=True)
         dist.barrier()
         dist.destroy_process_group()
     except BaseException:
@@ -63,7 +73,8 @@ def _worker(rank, world, port, errq, suite, seeds):
 
 
 def run(suite, world, seeds):
-    ctx = mp.get_context("fork")
+    # fork before anything touches a GPU; spawn when the ranks use one
+    ctx = mp.get_context("fork" if os.environ.get("BOLT_AMD_SOAK_DEVICE", "cpu") == "cpu" else "spawn")
     errq = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, errq, suite, seeds)) for r in range(world)]
