@@ -6,7 +6,8 @@ same seeded case on a context that
 spans the ranks, so arrays are sharded (ragged and empty slabs) and every
 exchange path runs -- swaps, sharded statistics, chunk moves (suite
 "oracle", tests/test_fuzz_oracle.py), indexing and its row exchanges
-("getitem", tests/test_getitem_fuzz.py), reshapes / squeeze / concatenate /
+("getitem", tests/test_getitem_fuzz.py), chunk chains ("chunk",
+tests/test_chunk_fuzz.py), reshapes / squeeze / concatenate /
 reductions / map / filter / stacks ("api", tests/test_api_fuzz.py) -- each
 compared with the oracle.
 
@@ -32,6 +33,9 @@ def _case_fn(suite):
     if suite == "getitem":
         from test_getitem_fuzz import test_getitem_fuzz
         return test_getitem_fuzz
+    if suite == "chunk":
+        from test_chunk_fuzz import test_chunk_fuzz
+        return test_chunk_fuzz
     from test_api_fuzz import test_api_fuzz
     return test_api_fuzz
 

@@ -1,6 +1,6 @@
 # Fuzz soak on one GPU: the seeded fuzz suites over seed ranges beyond the
 # suite's (BOLT_AMD_FUZZ_SEEDS), each stopping at its first failure.
-#   TAG=r05j ORACLE=200:2200 MEDIUM=240:1240 GETITEM=300:3300 API=200:1200 bash tools/gpu_fuzz_soak.sh
+#   TAG=r05j ORACLE=200:2200 MEDIUM=240:1240 GETITEM=300:3300 API=200:1200 CHUNK=200:1200 bash tools/gpu_fuzz_soak.sh
 set -o pipefail
 T=${TAG:-soak}
 mkdir -p gpurun_out
@@ -15,4 +15,5 @@ run oracle tests/test_fuzz_oracle.py ${ORACLE:-200:1200} &&
 run medium tests/test_gpu_fuzz_medium.py ${MEDIUM:-240:1240} &&
 run getitem tests/test_getitem_fuzz.py ${GETITEM:-300:3300} &&
 run api tests/test_api_fuzz.py ${API:-200:1200} &&
+run chunk tests/test_chunk_fuzz.py ${CHUNK:-200:1200} &&
 echo ALL_OK
