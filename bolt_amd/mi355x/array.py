@@ -106,6 +106,8 @@ def _move_plan(shape, perm, split):
     moved = [p for p in perm if shape[p] != 1]
     return (perm, int(split), tuple(shape[p] for p in perm), perm == tuple(range(len(shape))),
             moved == sorted(moved))
+
+
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
 _STAT_AXES = {}  # (shape, axis as given) -> (validated axis tuple, records after _align)
 

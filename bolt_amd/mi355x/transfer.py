@@ -159,9 +159,9 @@ def host_result(backend, nbytes, device):
     import torch
     host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     # torch's caching host allocator hands the same page-locked blocks out
-    # again: the check runs once per (block, size) (~1 us of a statistic's
-    # host path, profiles/r01_host_breakdown.log)
-    key = (host.data_ptr(), nbytes)
+    # again: the check runs once per (block, size, device) (~1 us of a
+    # statistic's host path, profiles/r01_host_breakdown.log)
+    key = (host.data_ptr(), nbytes, device.index)
     ok = _WRITABLE.get(key)
     if ok is None:
         ok = bool(writable(host))
@@ -171,7 +171,7 @@ def host_result(backend, nbytes, device):
     return host if ok else None
 
 
-_WRITABLE = {}  # (page-locked block address, bytes) -> kernels can store into it
+_WRITABLE = {}  # (page-locked block address, bytes, device) -> its kernels can store into it
 
 
 _STREAMS = {}  # device index -> torch Stream object of the last current stream seen
