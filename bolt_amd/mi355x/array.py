@@ -549,6 +549,7 @@ class BoltArrayMI355X(BoltArray):
         axis = tupleize(axis)
         swapped = self._align(axis)
         dev = swapped._data.device
+        func = F.user_fn(func)
         test_func = (lambda x: func((F.KeyTuple((0,) * len(axis)), x))) if with_keys else func
         if value_shape is None or dtype is None:
             try:
@@ -590,6 +591,7 @@ class BoltArrayMI355X(BoltArray):
         axis = tupleize(axis)
         swapped = self._align(axis)
         recs = swapped._records_tensor()
+        func = F.user_fn(func)
         keep = F.apply_batched(lambda v: F.to_device(func(v), v.device).reshape(()).to(bool), recs)
         mask = keep.cpu().numpy().reshape(-1) if keep is not None else np.zeros(0, bool)
         ctx = swapped._ctx
@@ -881,7 +883,8 @@ class BoltArrayMI355X(BoltArray):
         elif stat is not None and self._reduce_dtype_ok(func, stat):
             arr, _ = self._reduced(axis, stat)
         else:
-            arr = self._tree_reduce(func, axis)
+            from bolt_amd.mi355x.functional import user_fn
+            arr = self._tree_reduce(user_fn(func), axis)
         if arr.ndim == 0:
             arr = arr[()]
         if keepdims:

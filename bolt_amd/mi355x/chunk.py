@@ -447,6 +447,7 @@ class ChunkedArrayMI355X(object):
         """
         from bolt_amd.mi355x import functional as F
         dev = self._packed.device
+        func = F.user_fn(func)
         if value_shape is None or dtype is None:
             try:
                 mapped = F.to_device(func(F.random_like(self.plan, self._dtype, dev)), dev)
@@ -508,6 +509,7 @@ class ChunkedArrayMI355X(object):
         """
         from bolt_amd.local import BoltArrayLocal
         from bolt_amd.mi355x import functional as F
+        func = F.user_fn(func)
         g = self._geom
         es = self._dtype.itemsize
         lshape = local_shape(self._ctx, self._shape)

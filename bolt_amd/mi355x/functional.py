@@ -39,6 +39,39 @@ def numpy_dtype(tdtype):
     raise NotImplementedError("torch dtype %s has no numpy counterpart" % tdtype)
 
 
+def user_fn(func):
+    """``func`` as the mode hands it records: torch has no arithmetic for
+    uint16 / uint32 (2.10: add, comparisons, max, neg raise NotImplementedError),
+    where the reference's numpy records compute in the fixed-width type.  Such
+    tensors reach ``func`` widened to int32 / int64 (every value exact), and a
+    result in the widened type comes back in the record type: numpy's
+    wrap-around for + - * & | ^ <<, exact for comparisons, min / max and //.
+    Keys (``with_keys`` pairs) pass through; other dtypes are untouched."""
+    import torch
+    wide = {torch.uint16: torch.int32, torch.uint32: torch.int64}
+
+    def widen(a):
+        if isinstance(a, torch.Tensor) and a.dtype in wide:
+            return a.to(wide[a.dtype]), a.dtype
+        if isinstance(a, tuple) and not isinstance(a, KeyTuple):  # a (key, value) pair
+            parts = [widen(x) for x in a]
+            orig = next((o for _, o in parts if o is not None), None)
+            return type(a)(x for x, _ in parts) if type(a) is tuple else a, orig
+        return a, None
+
+    def wrapped(*args):
+        new, orig = [], None
+        for a in args:
+            w, o = widen(a)
+            new.append(w)
+            orig = orig or o
+        out = func(*new)
+        if orig is not None and isinstance(out, torch.Tensor) and out.dtype == wide[orig]:
+            return out.to(orig)
+        return out
+    return wrapped
+
+
 def view(buf, shape, dtype):
     """A uint8 buffer seen as a tensor of ``dtype`` and ``shape`` (no copy)."""
     shape = tuple(int(s) for s in shape)

@@ -131,6 +131,7 @@ class StackedArrayMI355X(object):
         and exceptions as the reference.  ``func`` gets torch tensors on the GPU."""
         import torch
         from bolt_amd.mi355x import functional as F
+        func = F.user_fn(func)
         ashape, atest, btest, bshape, dt = self._probe(func)
         dtype = np.dtype(dt)
         tdt = F.torch_dtype(dtype)

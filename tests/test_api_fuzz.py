@@ -23,7 +23,7 @@ from oracle import bolt_oracle as O
 NCASES = 200
 # a soak run takes other seeds: BOLT_AMD_FUZZ_SEEDS=start:stop (default 0:NCASES)
 _SEEDS = range(*[int(v) for v in os.environ.get("BOLT_AMD_FUZZ_SEEDS", "0:%d" % NCASES).split(":")])
-DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16]
+DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16, np.uint16]
 
 
 def _factor(rng, n, parts):

@@ -143,3 +143,16 @@ def test_swap_length1_value_axis(bctx):
     assert s.shape == (5, 3, 1) and s.split == 2         # bolt_amd
     assert _exact(s.toarray().reshape(5, 3), O.toarray(ws))
     assert _exact(bolt.array(np.zeros((3, 1)), bctx).T.toarray(), np.zeros((1, 3)))
+
+
+def test_transpose_all_key_array(bctx):
+    """An array whose every axis is a key (split = ndim): the reference's
+    transpose raises ValueError (Values.transpose(()) takes max() of an empty
+    sequence, bolt/utils.py:171); bolt_amd transposes the keys, as numpy
+    would (docs/HISTORY.md §4, reference bugs not kept, item 7)."""
+    x = np.arange(24, dtype=np.int16).reshape(2, 3, 4)
+    b = bolt.array(x, bctx, axis=(0, 1, 2))
+    for perm in ((2, 0, 1), (1, 0, 2), (2, 1, 0)):
+        t = b.transpose(perm)
+        assert t.split == 3 and _exact(t.toarray(), x.transpose(perm))
+    assert _exact(b.T.toarray(), x.T)

@@ -1,0 +1,284 @@
+"""Differential fuzz against the REFERENCE itself (build container only: it
+imports /root/reference through tests/golden/make_golden.py's fake Spark
+context and its old-numpy shims; nothing of it reaches the GPU box).
+
+Random arrays (extents 2-6, random splits and dtypes) go through the same
+random operation on the reference's Spark mode and on bolt_amd (the numpy
+test executor of the kernel contracts; the HIP kernels are held to that
+executor's bytes by the GPU suites): swap, transpose, chunk -> records ->
+unchunk, keys_to_values / values_to_keys, indexing, mean / var / std, sum /
+min / max, key / value reshape, concatenate, map, filter.  Data movement must
+be bit-exact, statistics within tests/golden_cases.stat_close's rule, and an
+operation the reference refuses must raise the same exception type here.  The
+reference behaviours bolt_amd does not keep (docs/HISTORY.md §4) are routed
+around: length-1 axes are not generated, records are compared in key order,
+paddings that trigger removepad's over-trim are not drawn, an array the
+reference builds but cannot collect must raise ValueError here, a transpose
+of an all-key array (which the reference cannot do) must be numpy's, and
+filter is compared in key order (the reference's sort=True).
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/reference_diff_fuzz.py 0 2000
+"""
+import os
+import sys
+import time
+import traceback
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(HERE, "tests", "golden"), os.path.join(HERE, "tests"), HERE]
+
+import make_golden  # noqa: E402,F401  (the reference, its shims, fakespark)
+import numpy as np  # noqa: E402
+
+import bolt as ref_bolt  # noqa: E402  (the reference)
+from fakerdd import FakeContext  # noqa: E402
+
+import bolt_amd  # noqa: E402
+import cpu_backend  # noqa: E402
+import golden_cases as G  # noqa: E402
+from test_chunk_fuzz import _chunk_args  # noqa: E402
+from test_getitem_fuzz import _index  # noqa: E402
+
+DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16, np.uint16]
+
+
+class Refused(Exception):
+    pass
+
+
+def ref_records(r):
+    return sorted(r._rdd.collect(), key=lambda kv: kv[0])
+
+
+def ref_array(r):
+    """The reference's array in key order (its sortByKey + collect); ValueError
+    when its records cannot fill the shape it declares."""
+    recs = ref_records(r)
+    try:
+        return np.asarray([v for _, v in recs]).reshape(r.shape)
+    except ValueError as e:
+        raise Refused("uncollectable: %s" % e)
+
+
+def same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and a.dtype == b.dtype and a.tobytes() == b.tobytes()
+
+
+def run_both(f_ref, f_ours):
+    """(ref result, our result) or (exception name, None) when both refuse alike."""
+    try:
+        rv = f_ref()
+        if hasattr(rv, "_rdd") and not hasattr(rv, "plan"):
+            ref_array(rv)  # an uncollectable array counts as refused (ValueError)
+    except Refused:
+        try:
+            ov = f_ours()
+            if hasattr(ov, "toarray"):
+                ov.toarray()
+        except ValueError:
+            return "refused", None
+        raise AssertionError("reference array cannot be collected; bolt_amd did not refuse")
+    except Exception as e:
+        try:
+            f_ours()
+        except Exception as e2:
+            assert type(e2).__name__ == type(e).__name__, (type(e).__name__, type(e2).__name__, e2)
+            return "raised " + type(e).__name__, None
+        raise AssertionError("reference raised %s (%s); bolt_amd did not" % (type(e).__name__, e))
+    return rv, f_ours()
+
+
+def check_array(rv, ov, what):
+    assert tuple(ov.shape) == tuple(rv.shape) and ov.split == rv.split, (what, ov.shape, rv.shape, ov.split, rv.split)
+    assert same(ov.toarray(), ref_array(rv)), what
+
+
+def check_chunked(rv, ov, what):
+    assert tuple(ov.shape) == tuple(rv.shape) and ov.split == rv.split, (what, ov.shape, rv.shape)
+    assert np.array_equal(ov.plan, rv.plan) and np.array_equal(ov.padding, rv.padding), (what, ov.plan, rv.plan)
+    got = list(ov.records())
+    want = ref_records(rv)
+    assert [tuple(k) for k, _ in got] == [tuple(k) for k, _ in want], what
+    for (k, gv), (_, wv) in zip(got, want):
+        assert same(gv, np.ascontiguousarray(wv)), (what, k)
+
+
+def one_case(seed, sc, ctx):
+    rng = np.random.default_rng(20000 + seed)
+    nd = int(rng.integers(2, 6))
+    shape = tuple(int(rng.integers(2, 7 if nd > 3 else 9)) for _ in range(nd))
+    split = int(rng.integers(1, nd + 1))
+    dtype = DTYPES[int(rng.integers(0, len(DTYPES)))]
+    if np.dtype(dtype).kind == "f":
+        x = (5 + 2 * rng.standard_normal(shape)).astype(dtype)
+    else:
+        x = rng.integers(0, 60, size=shape).astype(dtype)
+    axis = tuple(range(split))
+    npart = int(rng.integers(1, 5))
+    r = ref_bolt.array(x, sc, axis=axis, npartitions=npart)
+    o = bolt_amd.array(x, ctx, axis=axis)
+    check_array(r, o, "construct")
+    fam = ["swap", "transpose", "chunk", "getitem", "stat", "reduce", "reshape", "concat", "map", "filter"]
+    did = []
+    for _ in range(int(rng.integers(1, 4))):
+        f = fam[int(rng.integers(0, len(fam)))]
+        did.append(f)
+        nd, split = len(r.shape), r.split
+        if f == "swap":
+            kax = tuple(sorted(rng.choice(split, int(rng.integers(0, split + 1)), replace=False).tolist()))
+            vax = tuple(sorted(rng.choice(nd - split, int(rng.integers(0, nd - split + 1)), replace=False).tolist()))
+            if (len(kax) == split and not vax) or not (kax or vax):
+                continue
+            rv, ov = run_both(lambda: r.swap(kax, vax), lambda: o.swap(kax, vax))
+            if ov is not None:
+                check_array(rv, ov, ("swap", kax, vax))
+                if 1 not in rv.shape:
+                    r, o = rv, ov
+        elif f == "transpose":
+            perm = tuple(rng.permutation(nd).tolist())
+            if split == nd:
+                # the reference cannot transpose an all-key array (Values.transpose(())
+                # -> max() of an empty sequence, utils.py:171): a bug not kept
+                # (docs/HISTORY.md §4 item 7); bolt_amd gives numpy's transpose
+                try:
+                    r.transpose(perm)
+                    raise AssertionError("the reference transposed an all-key array")
+                except ValueError:
+                    pass
+                ot = o.transpose(perm)
+                assert ot.split == split and same(ot.toarray(), np.transpose(o.toarray(), perm)), ("T all-key", perm)
+                continue
+            rv, ov = run_both(lambda: r.transpose(perm), lambda: o.transpose(perm))
+            if ov is not None:
+                check_array(rv, ov, ("transpose", perm))
+                r, o = rv, ov
+        elif f == "chunk":
+            if split == nd:
+                continue
+            size, caxes, pad = _chunk_args(rng, r.shape[split:])
+            rv, ov = run_both(lambda: r.chunk(size, axis=caxes, padding=pad), lambda: o.chunk(size, axis=caxes, padding=pad))
+            if ov is None:
+                continue
+            check_chunked(rv, ov, ("chunk", size, caxes, pad))
+            if rng.random() < 0.5 and rv.split > 1:
+                k = (int(rng.integers(0, rv.split)),)
+                rv2, ov2 = run_both(lambda: rv.keys_to_values(k), lambda: ov.keys_to_values(k))
+                if ov2 is not None:
+                    check_chunked(rv2, ov2, ("k2v", k))
+                    rv, ov = rv2, ov2
+            elif len(rv.vshape) > 1:
+                v = (int(rng.integers(0, len(rv.vshape))),)
+                rv2, ov2 = run_both(lambda: rv.values_to_keys(v), lambda: ov.values_to_keys(v))
+                if ov2 is not None:
+                    check_chunked(rv2, ov2, ("v2k", v))
+                    rv, ov = rv2, ov2
+            ru, ou = rv.unchunk(), ov.unchunk()
+            check_array(ru, ou, "unchunk")
+        elif f == "getitem":
+            index = _index(rng, r.shape, split)
+            if index is None:
+                continue
+            rv, ov = run_both(lambda: r[index], lambda: o[index])
+            if ov is None:
+                continue
+            if hasattr(rv, "_rdd"):
+                check_array(rv, ov, ("getitem", index))
+            else:
+                assert type(ov).__name__ == type(rv).__name__ and same(ov, rv), ("getitem scalar", index)
+        elif f == "stat":
+            ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
+            name = ["mean", "var", "std"][int(rng.integers(0, 3))]
+            rv, ov = run_both(lambda: getattr(r, name)(axis=ax), lambda: getattr(o, name)(axis=ax))
+            if ov is None:
+                continue
+            a, w = np.asarray(ov), np.asarray(rv)
+            assert a.shape == w.shape and a.dtype == w.dtype, (name, a.shape, w.shape, a.dtype, w.dtype)
+            xa = o.toarray()
+            assert G.stat_close(a, w, G.truth_stat(xa, name, ax), w.dtype, xa, name), (name, ax)
+        elif f == "reduce":
+            ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
+            name = ["sum", "min", "max"][int(rng.integers(0, 3))]
+            rv, ov = run_both(lambda: getattr(r, name)(axis=ax), lambda: getattr(o, name)(axis=ax))
+            if ov is None:
+                continue
+            a = np.asarray(ov.toarray() if hasattr(ov, "toarray") else ov)
+            w = np.asarray(rv.toarray() if hasattr(rv, "toarray") else rv)
+            assert G.reduce_close(a, w, o.toarray(), "add" if name == "sum" else name, ax), (name, ax)
+        elif f == "reshape":
+            which = "keys" if rng.random() < 0.5 or split == nd else "values"
+            dims = r.shape[:split] if which == "keys" else r.shape[split:]
+            n = int(np.prod(dims))
+            parts = int(rng.integers(1, 4))
+            new = [1] * parts
+            k = n
+            for p in range(2, n + 1):
+                while k % p == 0:
+                    new[int(rng.integers(0, parts))] *= p
+                    k //= p
+            new = tuple(new)
+            if 1 in new:
+                continue
+            rv, ov = run_both(lambda: getattr(r, which).reshape(new), lambda: getattr(o, which).reshape(new))
+            if ov is not None:
+                check_array(rv, ov, ("reshape", which, new))
+                r, o = rv, ov
+        elif f == "concat":
+            cat = int(rng.integers(0, nd))
+            oshape = list(r.shape)
+            oshape[cat] = int(rng.integers(2, 4))
+            other = (np.arange(int(np.prod(oshape))) % 11).astype(r.dtype).reshape(oshape)
+            rv, ov = run_both(lambda: r.concatenate(other, axis=cat), lambda: o.concatenate(other, axis=cat))
+            if ov is not None:
+                check_array(rv, ov, ("concatenate", cat))
+        elif f == "map":
+            ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
+            rv, ov = run_both(lambda: r.map(lambda v: v * 2 + 1, axis=ax), lambda: o.map(lambda v: v * 2 + 1, axis=ax))
+            if ov is not None:
+                assert tuple(ov.shape) == tuple(rv.shape) and ov.split == rv.split, ("map", ax, ov.shape, rv.shape)
+                assert np.dtype(ov.dtype) == np.dtype(rv.dtype), ("map dtype", ov.dtype, rv.dtype)
+                assert same(ov.toarray(), ref_array(rv)), ("map", ax)
+        elif f == "filter":
+            ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
+            thr = float(np.median(r.toarray().astype(np.float64)))
+            srt = bool(rng.random() < 0.5)
+
+            def keep(v):
+                tot = v.double().sum() if hasattr(v, "double") else np.asarray(v).astype(np.float64).sum()
+                return float(tot) > thr * max(1, v.reshape(-1).shape[0])
+            # bolt_amd renumbers the kept records in key order whatever ``sort`` says;
+            # the reference's sort=False keeps its RDD's current order, which after
+            # a shuffle (a swap / transpose earlier in the chain) is the shuffle's
+            # (docs/HISTORY.md §4 item 8): compared with the reference's sort=True
+            rv, ov = run_both(lambda: r.filter(keep, axis=ax, sort=True), lambda: o.filter(keep, axis=ax, sort=srt))
+            if ov is not None:
+                assert tuple(ov.shape) == tuple(rv.shape) and ov.split == rv.split, ("filter", ax, ov.shape, rv.shape)
+                if rv.shape != (0,):
+                    assert same(ov.toarray(), ref_array(rv)), ("filter", ax)
+    return did
+
+
+def main(lo, hi):
+    cpu_backend.install()
+    ctx = bolt_amd.MI355XContext(device="cpu")
+    sc = FakeContext(4)
+    counts, bad = {}, []
+    t0 = time.time()
+    for seed in range(lo, hi):
+        try:
+            for f in one_case(seed, sc, ctx):
+                counts[f] = counts.get(f, 0) + 1
+        except Exception:
+            bad.append((seed, traceback.format_exc()[-1500:]))
+            if len(bad) >= 5:
+                break
+    print("seeds %d..%d: %d failed, operations compared %s, %.0f s"
+          % (lo, hi - 1, len(bad), dict(sorted(counts.items())), time.time() - t0))
+    for seed, tb in bad:
+        print("seed %d:\n%s" % (seed, tb))
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    a = [int(v) for v in sys.argv[1:3]] or [0, 200]
+    sys.exit(main(*a))
