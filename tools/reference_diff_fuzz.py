@@ -7,7 +7,9 @@ random operation on the reference's Spark mode and on bolt_amd (the numpy
 test executor of the kernel contracts; the HIP kernels are held to that
 executor's bytes by the GPU suites): swap, transpose, chunk -> records ->
 unchunk, keys_to_values / values_to_keys, indexing, mean / var / std, sum /
-min / max, key / value reshape, concatenate, map, filter.  Data movement must
+min / max (also with keepdims), reduce with numpy ufuncs, key / value reshape
+and transpose, swapaxes, concatenate, map, filter, first, astype, clip,
+stack -> map -> unstack, ChunkedArray.map.  Data movement must
 be bit-exact, statistics within tests/golden_cases.stat_close's rule, and an
 operation the reference refuses must raise the same exception type here.  The
 reference behaviours bolt_amd does not keep (docs/HISTORY.md §4) are routed
@@ -119,7 +121,8 @@ def one_case(seed, sc, ctx):
     r = ref_bolt.array(x, sc, axis=axis, npartitions=npart)
     o = bolt_amd.array(x, ctx, axis=axis)
     check_array(r, o, "construct")
-    fam = ["swap", "transpose", "chunk", "getitem", "stat", "reduce", "reshape", "concat", "map", "filter"]
+    fam = ["swap", "transpose", "chunk", "getitem", "stat", "reduce", "reshape", "concat", "map", "filter",
+           "swapaxes", "kvtranspose", "keepdims", "ufunc", "first", "astype", "clip", "stack", "chunkmap"]
     did = []
     for _ in range(int(rng.integers(1, 4))):
         f = fam[int(rng.integers(0, len(fam)))]
@@ -238,6 +241,83 @@ def one_case(seed, sc, ctx):
                 assert tuple(ov.shape) == tuple(rv.shape) and ov.split == rv.split, ("map", ax, ov.shape, rv.shape)
                 assert np.dtype(ov.dtype) == np.dtype(rv.dtype), ("map dtype", ov.dtype, rv.dtype)
                 assert same(ov.toarray(), ref_array(rv)), ("map", ax)
+        elif f == "swapaxes":
+            if nd < 2:
+                continue
+            a1, a2 = (int(v) for v in rng.choice(nd, 2, replace=False))
+            if split == nd:
+                continue  # an all-key array: the reference cannot transpose it (item 7)
+            rv, ov = run_both(lambda: r.swapaxes(a1, a2), lambda: o.swapaxes(a1, a2))
+            if ov is not None:
+                check_array(rv, ov, ("swapaxes", a1, a2))
+                r, o = rv, ov
+        elif f == "kvtranspose":
+            which = "keys" if rng.random() < 0.5 or split == nd else "values"
+            n = split if which == "keys" else nd - split
+            p = tuple(rng.permutation(n).tolist())
+            rv, ov = run_both(lambda: getattr(r, which).transpose(*p), lambda: getattr(o, which).transpose(*p))
+            if ov is not None:
+                check_array(rv, ov, (which + ".transpose", p))
+                r, o = rv, ov
+        elif f == "keepdims":
+            ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
+            name = ["sum", "mean", "max", "std"][int(rng.integers(0, 4))]
+            rv, ov = run_both(lambda: getattr(r, name)(axis=ax, keepdims=True),
+                              lambda: getattr(o, name)(axis=ax, keepdims=True))
+            if ov is None:
+                continue
+            a = np.asarray(ov.toarray() if hasattr(ov, "toarray") else ov)
+            w = np.asarray(rv.toarray() if hasattr(rv, "toarray") else rv)
+            assert a.shape == w.shape and a.dtype == w.dtype, (name, "keepdims", a.shape, w.shape)
+            xa = o.toarray()
+            if name in ("mean", "std"):
+                assert G.stat_close(a, w, G.truth_stat(xa, name, ax).reshape(w.shape), w.dtype, xa, name), name
+            else:
+                assert G.reduce_close(a, w, xa, "add" if name == "sum" else name, ax), name
+        elif f == "ufunc":
+            ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
+            kind = np.dtype(r.dtype).kind
+            ufs = [np.multiply, np.maximum, np.minimum, np.fmax, np.fmin] + (
+                [np.bitwise_and, np.bitwise_or, np.bitwise_xor, np.logical_and, np.logical_or] if kind in "iu" else [])
+            uf = ufs[int(rng.integers(0, len(ufs)))]
+            rv, ov = run_both(lambda: r.reduce(uf, axis=ax), lambda: o.reduce(uf, axis=ax))
+            if ov is None:
+                continue
+            a = np.asarray(ov.toarray() if hasattr(ov, "toarray") else ov)
+            w = np.asarray(rv.toarray() if hasattr(rv, "toarray") else rv)
+            fname = {np.multiply: "multiply"}.get(uf, uf.__name__)
+            assert G.reduce_close(a, w, o.toarray(), fname, ax), ("reduce", uf.__name__, ax)
+        elif f == "first":
+            rv, ov = run_both(lambda: r.first(), lambda: o.first())
+            if ov is not None:
+                assert same(np.asarray(ov), np.asarray(rv)), "first"
+        elif f == "astype":
+            dt = [np.float64, np.int32, np.uint8, np.float32][int(rng.integers(0, 4))]
+            rv, ov = run_both(lambda: r.astype(dt), lambda: o.astype(dt))
+            if ov is not None:
+                check_array(rv, ov, ("astype", dt))
+                r, o = rv, ov
+        elif f == "clip":
+            lo_, hi_ = sorted(float(v) for v in rng.integers(0, 60, 2))
+            rv, ov = run_both(lambda: r.clip(lo_, hi_), lambda: o.clip(lo_, hi_))
+            if ov is not None:
+                check_array(rv, ov, ("clip", lo_, hi_))
+        elif f == "stack":
+            size = int(rng.integers(1, 5))
+            rv, ov = run_both(lambda: r.stack(size).map(lambda v: v + 1).unstack(),
+                              lambda: o.stack(size).map(lambda v: v + 1).unstack())
+            if ov is not None:
+                assert tuple(ov.shape) == tuple(rv.shape) and ov.split == rv.split, ("stack", ov.shape, rv.shape)
+                assert same(ov.toarray(), ref_array(rv)), ("stack", size)
+        elif f == "chunkmap":
+            if split == nd:
+                continue
+            size, caxes, pad = _chunk_args(rng, r.shape[split:])
+            rv, ov = run_both(lambda: r.chunk(size, axis=caxes, padding=pad).map(lambda v: v * 3 + 2),
+                              lambda: o.chunk(size, axis=caxes, padding=pad).map(lambda v: v * 3 + 2))
+            if ov is not None:
+                check_chunked(rv, ov, ("chunk.map", size, caxes, pad))
+                check_array(rv.unchunk(), ov.unchunk(), "chunk.map unchunk")
         elif f == "filter":
             ax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))
             thr = float(np.median(r.toarray().astype(np.float64)))
