@@ -42,6 +42,10 @@ from test_chunk_fuzz import _chunk_args  # noqa: E402
 from test_getitem_fuzz import _index  # noqa: E402
 
 DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16, np.uint16]
+# BOLT_AMD_DIFF_MIN_EXTENT=1 also draws length-1 axes, around which the
+# reference's swaps misbehave (docs/HISTORY.md §4 item 6): a survey, not a gate
+MIN_EXTENT = int(os.environ.get("BOLT_AMD_DIFF_MIN_EXTENT", "2"))
+CATALOGUE = os.environ.get("BOLT_AMD_DIFF_CATALOGUE") == "1"  # list every difference, by message
 
 
 class Refused(Exception):
@@ -109,7 +113,7 @@ def check_chunked(rv, ov, what):
 def one_case(seed, sc, ctx):
     rng = np.random.default_rng(20000 + seed)
     nd = int(rng.integers(2, 6))
-    shape = tuple(int(rng.integers(2, 7 if nd > 3 else 9)) for _ in range(nd))
+    shape = tuple(int(rng.integers(MIN_EXTENT, 7 if nd > 3 else 9)) for _ in range(nd))
     split = int(rng.integers(1, nd + 1))
     dtype = DTYPES[int(rng.integers(0, len(DTYPES)))]
     if np.dtype(dtype).kind == "f":
@@ -350,8 +354,15 @@ def main(lo, hi):
                 counts[f] = counts.get(f, 0) + 1
         except Exception:
             bad.append((seed, traceback.format_exc()[-1500:]))
-            if len(bad) >= 5:
+            if len(bad) >= 5 and not CATALOGUE:
                 break
+    if CATALOGUE:
+        kinds = {}
+        for seed, tb in bad:
+            kinds.setdefault(tb.strip().splitlines()[-1][:160], []).append(seed)
+        for k, seeds in sorted(kinds.items(), key=lambda kv: -len(kv[1])):
+            print("%5d  e.g. seed %d  %s" % (len(seeds), seeds[0], k))
+        bad = bad[:3]
     print("seeds %d..%d: %d failed, operations compared %s, %.0f s"
           % (lo, hi - 1, len(bad), dict(sorted(counts.items())), time.time() - t0))
     for seed, tb in bad:
