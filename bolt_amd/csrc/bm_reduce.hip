@@ -656,6 +656,7 @@ __global__ void __launch_bounds__(kThreads)
 // ------------------------------------------------------------------ rows --
 struct RowsDesc {
   int64_t O, R;
+  int64_t P;       // elements between row starts (R, or a padded row pitch >= R)
   int64_t rchunk;
   FastDiv nchunks;
   int64_t nitems;  // O * nchunks
@@ -680,7 +681,7 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t c = item - (int64_t)o * (int64_t)d.nchunks.d;
   const int64_t r_lo = c * d.rchunk;
   const int64_t r_hi = min(d.R, r_lo + d.rchunk);
-  const T *row = src + (int64_t)o * d.R;
+  const T *row = src + (int64_t)o * d.P;
 
   Acc<M_MEAN> acc;
   acc.init();
@@ -950,7 +951,7 @@ __global__ void __launch_bounds__(kThreads)
   const int64_t c = item - (int64_t)o * (int64_t)d.nchunks.d;
   const int64_t r_lo = c * d.rchunk;
   const int64_t r_hi = min(d.R, r_lo + d.rchunk);
-  const T *row = src + (int64_t)o * d.R;
+  const T *row = src + (int64_t)o * d.P;
   int64_t s1 = 0;
   uint64_t s2 = 0;
   const int64_t stride = 64 * VEC;
@@ -1194,14 +1195,15 @@ struct RedPlan {
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
+RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src, int64_t P) {
   RedPlan p{};
   const int es = dtype_size(dt);
   const bool al16 = src == nullptr || ((uintptr_t)src % 16) == 0;
   if (I == 1) {
     p.rows = true;
     int vec = 16 / es;
-    while (vec > 1 && !(R % vec == 0 && (src == nullptr || ((uintptr_t)src % (vec * es)) == 0))) vec >>= 1;
+    while (vec > 1 && !(R % vec == 0 && P % vec == 0 && (src == nullptr || ((uintptr_t)src % (vec * es)) == 0)))
+      vec >>= 1;
     p.vec = vec;
     const int64_t target_waves = 8192;
     int64_t nch = 1;
@@ -1251,10 +1253,11 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src) {
 
 // exact integer var / std: the same grids as the float kernels
 template <typename T>
-int launch_int_mom(const RedPlan &p, const T *s, int64_t O, int64_t R, int64_t I, Sink sk, hipStream_t st) {
+int launch_int_mom(const RedPlan &p, const T *s, int64_t O, int64_t R, int64_t P, int64_t I, Sink sk,
+                   hipStream_t st) {
   if (p.rows) {
     RowsDesc d;
-    d.O = O; d.R = R; d.rchunk = p.rchunk;
+    d.O = O; d.R = R; d.P = P; d.rchunk = p.rchunk;
     d.nchunks = make_fastdiv((uint64_t)p.nchunks);
     d.nitems = O * p.nchunks;
     const int64_t blocks = cdiv(d.nitems, kThreads / 64);
@@ -1299,15 +1302,15 @@ template <int MODE> size_t cols_lds_bytes(int nph, int vec) {
 }
 
 template <typename T, int MODE>
-int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64_t I, Sink sk,
+int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64_t P, int64_t I, Sink sk,
                   hipStream_t st) {
   const T *s = (const T *)src;
   if constexpr (MODE == M_MOM && small_int<T>()) {
-    return launch_int_mom<T>(p, s, O, R, I, sk, st);
+    return launch_int_mom<T>(p, s, O, R, P, I, sk, st);
   }
   if (p.rows) {
     RowsDesc d;
-    d.O = O; d.R = R; d.rchunk = p.rchunk;
+    d.O = O; d.R = R; d.P = P; d.rchunk = p.rchunk;
     d.nchunks = make_fastdiv((uint64_t)p.nchunks);
     d.nitems = O * p.nchunks;
     const int64_t blocks = cdiv(d.nitems, kThreads / 64);
@@ -1347,26 +1350,26 @@ int launch_main_t(const RedPlan &p, const void *src, int64_t O, int64_t R, int64
 }
 
 template <int MODE>
-int launch_main_m(int dt, const RedPlan &p, const void *src, int64_t O, int64_t R, int64_t I,
+int launch_main_m(int dt, const RedPlan &p, const void *src, int64_t O, int64_t R, int64_t P, int64_t I,
                   Sink sk, hipStream_t st) {
   switch (dt) {
     case BM_BOOL:
-    case BM_U8: return launch_main_t<uint8_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_I8: return launch_main_t<int8_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_U16: return launch_main_t<uint16_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_I16: return launch_main_t<int16_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_U32: return launch_main_t<uint32_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_I32: return launch_main_t<int32_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_U64: return launch_main_t<uint64_t, MODE>(p, src, O, R, I, sk, st);
-    case BM_I64: return launch_main_t<int64_t, MODE>(p, src, O, R, I, sk, st);
+    case BM_U8: return launch_main_t<uint8_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_I8: return launch_main_t<int8_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_U16: return launch_main_t<uint16_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_I16: return launch_main_t<int16_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_U32: return launch_main_t<uint32_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_I32: return launch_main_t<int32_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_U64: return launch_main_t<uint64_t, MODE>(p, src, O, R, P, I, sk, st);
+    case BM_I64: return launch_main_t<int64_t, MODE>(p, src, O, R, P, I, sk, st);
     case BM_F16:
-      if constexpr (!int_only_mode<MODE>()) return launch_main_t<_Float16, MODE>(p, src, O, R, I, sk, st);
+      if constexpr (!int_only_mode<MODE>()) return launch_main_t<_Float16, MODE>(p, src, O, R, P, I, sk, st);
       break;
     case BM_F32:
-      if constexpr (!int_only_mode<MODE>()) return launch_main_t<float, MODE>(p, src, O, R, I, sk, st);
+      if constexpr (!int_only_mode<MODE>()) return launch_main_t<float, MODE>(p, src, O, R, P, I, sk, st);
       break;
     case BM_F64:
-      if constexpr (!int_only_mode<MODE>()) return launch_main_t<double, MODE>(p, src, O, R, I, sk, st);
+      if constexpr (!int_only_mode<MODE>()) return launch_main_t<double, MODE>(p, src, O, R, P, I, sk, st);
       break;
     default: break;
   }
@@ -1375,23 +1378,23 @@ int launch_main_m(int dt, const RedPlan &p, const void *src, int64_t O, int64_t 
 }
 
 int launch_main(int mode, int dt, const RedPlan &p, const void *src, int64_t O, int64_t R,
-                int64_t I, Sink sk, hipStream_t st) {
+                int64_t P, int64_t I, Sink sk, hipStream_t st) {
   switch (mode) {
-    case M_MEAN: return launch_main_m<M_MEAN>(dt, p, src, O, R, I, sk, st);
-    case M_MOM: return launch_main_m<M_MOM>(dt, p, src, O, R, I, sk, st);
-    case M_FSUM: return launch_main_m<M_FSUM>(dt, p, src, O, R, I, sk, st);
-    case M_ISUM: return launch_main_m<M_ISUM>(dt, p, src, O, R, I, sk, st);
-    case M_MAX: return launch_main_m<M_MAX>(dt, p, src, O, R, I, sk, st);
-    case M_MIN: return launch_main_m<M_MIN>(dt, p, src, O, R, I, sk, st);
-    case M_FPROD: return launch_main_m<M_FPROD>(dt, p, src, O, R, I, sk, st);
-    case M_IPROD: return launch_main_m<M_IPROD>(dt, p, src, O, R, I, sk, st);
-    case M_LAND: return launch_main_m<M_LAND>(dt, p, src, O, R, I, sk, st);
-    case M_BAND: return launch_main_m<M_BAND>(dt, p, src, O, R, I, sk, st);
-    case M_BOR: return launch_main_m<M_BOR>(dt, p, src, O, R, I, sk, st);
-    case M_BXOR: return launch_main_m<M_BXOR>(dt, p, src, O, R, I, sk, st);
-    case M_FMAX: return launch_main_m<M_FMAX>(dt, p, src, O, R, I, sk, st);
-    case M_FMIN: return launch_main_m<M_FMIN>(dt, p, src, O, R, I, sk, st);
-    default: return launch_main_m<M_OR>(dt, p, src, O, R, I, sk, st);
+    case M_MEAN: return launch_main_m<M_MEAN>(dt, p, src, O, R, P, I, sk, st);
+    case M_MOM: return launch_main_m<M_MOM>(dt, p, src, O, R, P, I, sk, st);
+    case M_FSUM: return launch_main_m<M_FSUM>(dt, p, src, O, R, P, I, sk, st);
+    case M_ISUM: return launch_main_m<M_ISUM>(dt, p, src, O, R, P, I, sk, st);
+    case M_MAX: return launch_main_m<M_MAX>(dt, p, src, O, R, P, I, sk, st);
+    case M_MIN: return launch_main_m<M_MIN>(dt, p, src, O, R, P, I, sk, st);
+    case M_FPROD: return launch_main_m<M_FPROD>(dt, p, src, O, R, P, I, sk, st);
+    case M_IPROD: return launch_main_m<M_IPROD>(dt, p, src, O, R, P, I, sk, st);
+    case M_LAND: return launch_main_m<M_LAND>(dt, p, src, O, R, P, I, sk, st);
+    case M_BAND: return launch_main_m<M_BAND>(dt, p, src, O, R, P, I, sk, st);
+    case M_BOR: return launch_main_m<M_BOR>(dt, p, src, O, R, P, I, sk, st);
+    case M_BXOR: return launch_main_m<M_BXOR>(dt, p, src, O, R, P, I, sk, st);
+    case M_FMAX: return launch_main_m<M_FMAX>(dt, p, src, O, R, P, I, sk, st);
+    case M_FMIN: return launch_main_m<M_FMIN>(dt, p, src, O, R, P, I, sk, st);
+    default: return launch_main_m<M_OR>(dt, p, src, O, R, P, I, sk, st);
   }
 }
 
@@ -1480,13 +1483,14 @@ size_t ws_bytes_for(int mode, const RedPlan &p, int64_t nout) {
 }
 
 // Shared body of bm_reduce / bm_reduce_state.
+// P: row pitch in elements (rows reductions, I == 1); R for a dense input.
 int run_reduce(int stat, const void *src, int dt, int64_t O, int64_t R, int64_t I, Sink sk,
-               void *ws, size_t ws_bytes, hipStream_t st, const char *who) {
+               void *ws, size_t ws_bytes, hipStream_t st, const char *who, int64_t P) {
   const int mode = mode_of(stat, dt);
-  const RedPlan p = plan_reduce(dt, O, R, I, src);
+  const RedPlan p = plan_reduce(dt, O, R, I, src, P);
   const int64_t nout = O * I;
   if (p.nchunks <= 1) {
-    int rc = launch_main(mode, dt, p, src, O, R, I, sk, st);
+    int rc = launch_main(mode, dt, p, src, O, R, P, I, sk, st);
     if (rc) return rc;
     return check_launch(who);
   }
@@ -1503,7 +1507,7 @@ int run_reduce(int stat, const void *src, int dt, int64_t O, int64_t R, int64_t 
   part.p1 = w1;
   part.p2 = w1 + (size_t)p.nchunks * nout;  // var / std pivots (ws_bytes_for reserves the plane)
   part.shifted = mode == M_MOM;
-  int rc = launch_main(mode, dt, p, src, O, R, I, part, st);
+  int rc = launch_main(mode, dt, p, src, O, R, P, I, part, st);
   if (rc) return rc;
   CombDesc cd{};
   cd.nout = nout;
@@ -1529,27 +1533,29 @@ extern "C" int bm_reduce_workspace_bytes(int stat, int in_dtype, int64_t O, int6
   // The plan depends on the pointer only through the vector width; reserve
   // for both the 16-B-aligned plan and the scalar (unaligned) plan.
   const int mode = mode_of(stat, in_dtype);
-  const size_t a = ws_bytes_for(mode, plan_reduce(in_dtype, O, R, I, nullptr), O * I);
-  const size_t b = ws_bytes_for(mode, plan_reduce(in_dtype, O, R, I, (const void *)1), O * I);
+  const size_t a = ws_bytes_for(mode, plan_reduce(in_dtype, O, R, I, nullptr, R), O * I);
+  const size_t b = ws_bytes_for(mode, plan_reduce(in_dtype, O, R, I, (const void *)1, R), O * I);
   *bytes = a > b ? a : b;
   return BM_OK;
 }
 
-extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int64_t R, int64_t I,
-                         void *out, int out_dtype, void *workspace, size_t workspace_bytes,
-                         void *stream) {
-  int rc = check_args(stat, in_dtype, O, R, I, "bm_reduce");
+namespace {
+// bm_reduce / bm_reduce_rows: validation, then run_reduce into `out`.
+int reduce_to_out(int stat, const void *src, int in_dtype, int64_t O, int64_t R, int64_t I, int64_t P,
+                  void *out, int out_dtype, void *workspace, size_t workspace_bytes, void *stream,
+                  const char *who) {
+  int rc = check_args(stat, in_dtype, O, R, I, who);
   if (rc) return rc;
-  if (!src || !out) { bm_set_error("bm_reduce: null pointer"); return BM_E_ARG; }
+  if (!src || !out) { bm_set_error("%s: null pointer", who); return BM_E_ARG; }
   const int mode = mode_of(stat, in_dtype);
   if (!out_dtype_ok(stat, mode, in_dtype, out_dtype)) {
-    bm_set_error("bm_reduce: out_dtype %d does not fit stat %d on dtype %d (float for statistics and "
+    bm_set_error("%s: out_dtype %d does not fit stat %d on dtype %d (float for statistics and "
                  "float sums / products, bool for logical and / or, else the input dtype)",
-                 out_dtype, stat, in_dtype);
+                 who, out_dtype, stat, in_dtype);
     return BM_E_ARG;
   }
   if (is_float(in_dtype) && (mode == M_BAND || mode == M_BOR || mode == M_BXOR)) {
-    bm_set_error("bm_reduce: bitwise reductions need an integer or bool dtype");
+    bm_set_error("%s: bitwise reductions need an integer or bool dtype", who);
     return BM_E_ARG;
   }
   Sink sk{};
@@ -1558,7 +1564,26 @@ extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int
   sk.stat = stat;
   sk.final_out = 1;
   return run_reduce(stat, src, in_dtype, O, R, I, sk, workspace, workspace_bytes,
-                    (hipStream_t)stream, "bm_reduce");
+                    (hipStream_t)stream, who, P);
+}
+}  // namespace
+
+extern "C" int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int64_t R, int64_t I,
+                         void *out, int out_dtype, void *workspace, size_t workspace_bytes,
+                         void *stream) {
+  return reduce_to_out(stat, src, in_dtype, O, R, I, R, out, out_dtype, workspace, workspace_bytes,
+                       stream, "bm_reduce");
+}
+
+extern "C" int bm_reduce_rows(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
+                              int64_t row_pitch, void *out, int out_dtype, void *workspace,
+                              size_t workspace_bytes, void *stream) {
+  if (row_pitch < R) {
+    bm_set_error("bm_reduce_rows: row_pitch %lld < row length %lld", (long long)row_pitch, (long long)R);
+    return BM_E_ARG;
+  }
+  return reduce_to_out(stat, src, in_dtype, O, R, 1, row_pitch, out, out_dtype, workspace, workspace_bytes,
+                       stream, "bm_reduce_rows");
 }
 
 extern "C" int bm_reduce_state_bytes(int stat, int in_dtype, int64_t nout, size_t *bytes) {
@@ -1585,7 +1610,7 @@ extern "C" int bm_reduce_state(int stat, const void *src, int in_dtype, int64_t 
   sk.p0 = (double *)state;
   sk.p1 = (double *)state + nout;
   return run_reduce(stat, src, in_dtype, O, R, I, sk, workspace, workspace_bytes,
-                    (hipStream_t)stream, "bm_reduce_state");
+                    (hipStream_t)stream, "bm_reduce_state", R);
 }
 
 extern "C" int bm_reduce_combine(int stat, int in_dtype, const void *states, const int64_t *counts,

@@ -46,6 +46,8 @@ SIGNATURES = {
                                              _c.c_int64, _c.POINTER(_c.c_size_t)]),
     "bm_reduce": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64,
                              _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    "bm_reduce_rows": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int64,
+                                  _c.c_void_p, _c.c_int, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     "bm_reduce_state_bytes": (_c.c_int, [_c.c_int, _c.c_int, _c.c_int64, _c.POINTER(_c.c_size_t)]),
     "bm_reduce_state": (_c.c_int, [_c.c_int, _c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64,
                                    _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p]),

@@ -304,6 +304,14 @@ class HipBackend(object):
         if rc:
             _lib.check(rc, "bm_reduce")
 
+    def reduce_rows(self, stat, src, code, O, R, pitch, out, out_code):
+        """reduce over O rows of R elements that start ``pitch`` elements apart."""
+        ws, nws = self._workspace(stat, code, O, R, 1, src.device)
+        rc = self.lib.bm_reduce_rows(stat, src.data_ptr(), code, O, R, pitch, out.data_ptr(), out_code,
+                                     ws.data_ptr() if ws is not None else None, nws, raw_stream(src.device))
+        if rc:
+            _lib.check(rc, "bm_reduce_rows")
+
     def state_bytes(self, stat, code, nout):
         n = ctypes.c_size_t(0)
         _lib.check(self.lib.bm_reduce_state_bytes(stat, code, nout, ctypes.byref(n)), "bm_reduce_state_bytes")

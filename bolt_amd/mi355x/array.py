@@ -17,6 +17,7 @@ Operations and what replaces the Spark machinery:
   toarray / tolocal: D2H (+ all_gather of the slabs).
 """
 import functools
+import os
 
 import numpy as np
 
@@ -106,6 +107,52 @@ def _move_plan(shape, perm, split):
     moved = [p for p in perm if shape[p] != 1]
     return (perm, int(split), tuple(shape[p] for p in perm), perm == tuple(range(len(shape))),
             moved == sorted(moved))
+
+
+# Row pitch of transposed results.  A transpose writes its destination rows in
+# 256-B tile segments; rows whose length is not a multiple of the 128-B line
+# start mid-line every other row (C2's 2000 float32 = 8000 B), so neighbouring
+# tiles write halves of the same lines.  Such a result is stored with its rows
+# padded to a 1-KiB multiple (8192 B): the C2 transpose 0.722 -> 0.674 ms and
+# its time-axis statistics 0.312 -> 0.297 ms (profiles/r05r_tpitch.log).
+# Statistics over the last axis read the padded rows in place
+# (bm_reduce_rows); any other use compacts the rows once (_compact).
+ROW_PITCH = os.environ.get("BOLT_AMD_ROW_PITCH", "1") != "0"
+_PITCH_MIN_ROW = 4096            # bytes: shorter rows are not padded
+_PITCH_ALIGN = 1024              # bytes: padded rows start on this boundary
+_PITCH_LINE = 128                # bytes: rows of a multiple of this stay dense
+_PITCH_PAD_DIV = 32              # at most 1/32 of a row is padding
+_PITCH_MAX_BYTES = 16 << 30      # larger results stay dense (compaction needs a second copy)
+_PITCH_PLANS = {}  # (_move_plan, itemsize) -> None | pitched copy plan
+
+
+def _pitch_plan(mv, shape, es):
+    """The pitched copy for _move_plan ``mv`` of an array of ``shape``, or None:
+    (pitch in elements, rows, output shape, source strides, pitched
+    destination strides), all in elements."""
+    perm, _, new_shape, _, _ = mv
+    nd = len(new_shape)
+    if nd < 2 or perm[-1] == nd - 1:
+        return None
+    R = new_shape[-1]
+    rb = R * es
+    if rb < _PITCH_MIN_ROW or rb % _PITCH_LINE == 0:
+        return None
+    pb = -(-rb // _PITCH_ALIGN) * _PITCH_ALIGN
+    if (pb - rb) * _PITCH_PAD_DIV > rb or pb % es:
+        return None
+    P = pb // es
+    rows = int(np.prod(new_shape[:-1], dtype=np.int64))
+    if rows * pb > _PITCH_MAX_BYTES or rows < 2:
+        return None
+    sstr = [1] * len(shape)
+    for k in range(len(shape) - 2, -1, -1):
+        sstr[k] = sstr[k + 1] * shape[k + 1]
+    dstr = [1] * nd
+    dstr[nd - 2] = P
+    for k in range(nd - 3, -1, -1):
+        dstr[k] = dstr[k + 1] * new_shape[k + 1]
+    return P, rows, list(new_shape), [sstr[p] for p in perm], dstr
 
 
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
@@ -234,9 +281,34 @@ class BoltArrayMI355X(BoltArray):
                             _ordered=True, _ctx=self._ctx, _npartitions=self._npartitions)
         return new
 
+    def __getattr__(self, name):
+        # only reached for attributes not set: a row-padded array's records
+        # (see ROW_PITCH) are compacted the first time anything needs them dense
+        if name == "_data" and "_pbuf" in self.__dict__:
+            return self._compact()
+        raise AttributeError("'%s' object has no attribute '%s'" % (type(self).__name__, name))
+
+    def _compact(self):
+        """Dense records of a row-padded array (one strided copy on the GPU)."""
+        d = self.__dict__
+        pbuf, P = d["_pbuf"], d["_pitch"]
+        es = self._dtype.itemsize
+        R = self._shape[-1]
+        rows = int(np.prod(self._shape[:-1], dtype=np.int64))
+        data = _empty(rows * R * es, pbuf.device)
+        backend_for(pbuf.device).copy_strided(pbuf, 0, data, 0, [rows, R], [P, 1], [R, 1], es)
+        d["_data"] = data
+        del d["_pbuf"], d["_pitch"]
+        return data
+
+    @property
+    def _device(self):
+        d = self.__dict__
+        return (d["_pbuf"] if "_pbuf" in d else d["_data"]).device
+
     @property
     def _backend(self):
-        return backend_for(self._data.device)
+        return backend_for(self._device)
 
     @property
     def _local_shape(self):
@@ -307,6 +379,26 @@ class BoltArrayMI355X(BoltArray):
             # bytes are already the result's (across GPUs the leading axis,
             # hence every slab, stays put)
             data = self._data
+        elif ROW_PITCH and self._ctx.world_size == 1:
+            es = self._dtype.itemsize
+            key = (mv, es)
+            pp = _PITCH_PLANS.get(key, False)
+            if pp is False:
+                pp = _pitch_plan(mv, self._shape, es)
+                if len(_PITCH_PLANS) > 4096:
+                    _PITCH_PLANS.clear()
+                _PITCH_PLANS[key] = pp
+            src = self._data
+            if pp is not None:
+                P, rows, oshape, sstr, dstr = pp
+                pbuf = _empty(rows * P * es, src.device)
+                backend_for(src.device).copy_strided(src, 0, pbuf, 0, oshape, sstr, dstr, es)
+                new = self._derive(None, new_shape, split)
+                d = new.__dict__
+                del d["_data"]
+                d["_pbuf"], d["_pitch"] = pbuf, P
+                return new
+            data = permute_sharded(self._ctx, backend_for(src.device), src, self._shape, perm, es)
         else:
             data = permute_sharded(self._ctx, backend_for(self._data.device), self._data, self._shape, perm,
                                    self._dtype.itemsize)
@@ -769,6 +861,17 @@ class BoltArrayMI355X(BoltArray):
                 _REDUCE_PLANS.clear()
             _REDUCE_PLANS[pkey] = plan
         axset, kept, out_shape, out_dtype, code, ocode, perm, O, R, I, nloc, loc_out, nout = plan
+        pbuf = self.__dict__.get("_pbuf")
+        if pbuf is not None and perm is None and I == 1 and R == lshape[-1] and nloc:
+            # last-axis statistic of a row-padded array: read the rows in place
+            be = backend_for(pbuf.device)
+            host = host_result(be, nout * out_dtype.itemsize, pbuf.device)
+            if host is not None:
+                be.reduce_rows(stat, pbuf, code, O, R, self._pitch, host, ocode)
+                return finish_host_result(host, pbuf.device, out_dtype, out_shape), out_dtype
+            out = _empty(nout * out_dtype.itemsize, pbuf.device)
+            be.reduce_rows(stat, pbuf, code, O, R, self._pitch, out, ocode)
+            return to_host(out, out_dtype, out_shape), out_dtype
         be = self._backend
         dev = self._data.device
         es = self._dtype.itemsize

@@ -248,6 +248,21 @@ int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
               size_t workspace_bytes, void *stream);
 
 /*
+ * bm_reduce over rows of a padded layout (I = 1): row o is the R elements at
+ * src + o * row_pitch (row_pitch >= R, in elements; the pad is never read).
+ * The per-record statistics of a transposed result -- mean / std over the
+ * time axis after swap((0,),(0,1)), bolt/spark/array.py:284-334 over
+ * statcounter.py -- when the swap wrote its rows at a line-aligned pitch
+ * (a row of 2000 float32 at 8000 B starts 64 B into a line every other row;
+ * padded to 8192 B the transpose and this read both run whole lines).
+ * Results identical to bm_reduce on the compacted rows; the same workspace
+ * (bm_reduce_workspace_bytes with I = 1 covers every pitch).
+ */
+int bm_reduce_rows(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
+                   int64_t row_pitch, void *out, int out_dtype, void *workspace,
+                   size_t workspace_bytes, void *stream);
+
+/*
  * Partial reduction state for the multi-GPU merge (the per-partition
  * StatCounter of array.py:321-322).  `state` receives, for O*I outputs:
  *   MEAN/VAR/STD: two float64 planes, mean[O*I] then M2[O*I] (count = R);

@@ -164,6 +164,11 @@ class CpuBackend(object):
         x = _np(src).view(_CODES[code]).reshape(O, R, I)
         self._finish(stat, code, self._planes(stat, code, x), float(R), out, out_code)
 
+    def reduce_rows(self, stat, src, code, O, R, pitch, out, out_code):
+        assert pitch >= R
+        x = _np(src).view(_CODES[code])[:O * pitch].reshape(O, pitch)[:, :R].reshape(O, R, 1)
+        self._finish(stat, code, self._planes(stat, code, x), float(R), out, out_code)
+
     def state_bytes(self, stat, code, nout):
         mom = stat in (STAT_VAR, STAT_STD)  # max / min / sum / mean: one 8-byte plane
         return (2 if mom else 1) * nout * 8

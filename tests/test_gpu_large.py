@@ -176,7 +176,13 @@ def test_stats_full_size_c2(gpu_ctx):
     import torch
     b, raw = _shard(gpu_ctx, (2000, 512, 512), np.float32, 1, 5)
     s = b.swap((0,), (0, 1))
+    assert "_pbuf" in s.__dict__ and s._pitch == 2048  # 8000-B rows stored at an 8192-B pitch
     m, sd = s.mean(axis=2), s.std(axis=2)
+    assert "_pbuf" in s.__dict__  # read in place (bm_reduce_rows)
+    d = b.swap((0,), (0, 1))
+    d._compact()
+    assert d.mean(axis=2).tobytes() == m.tobytes() and d.std(axis=2).tobytes() == sd.tobytes()
+    del d
     x = raw.view(torch.float32).reshape(2000, 512 * 512).double()
     mu = x.mean(0)
     var = ((x - mu) ** 2).mean(0)

@@ -1,0 +1,225 @@
+"""Row-padded transposed results (bolt_amd/mi355x/array.py, ROW_PITCH).
+
+A swap / transpose whose output rows are not a whole number of 128-B lines is
+stored with padded rows; statistics over the last axis read them in place
+(bm_reduce_rows) and every other use compacts them first.  Results must be
+the dense layout's: statistics against numpy (float64 truth within
+golden_cases.reduce_close for float sums, exact otherwise), data movement
+bit-exact.  The size thresholds are lowered here (``small_pitch``) so that the
+small arrays of the seeded suites take the padded path too; the oracle suites
+(tests/test_fuzz_oracle.py, test_api_fuzz.py, test_getitem_fuzz.py,
+test_chunk_fuzz.py) then run again over padded swap results.  Runs on the CPU
+test executor and (marker ``gpu``) on the HIP kernels.
+"""
+import numpy as np
+import pytest
+
+import bolt_amd as bolt
+import bolt_amd.mi355x.array as A
+import golden_cases as G
+
+
+@pytest.fixture
+def small_pitch(monkeypatch):
+    """Pad every transposed row that is not a multiple of 16 B, to 64 B."""
+    monkeypatch.setattr(A, "_PITCH_MIN_ROW", 1)
+    monkeypatch.setattr(A, "_PITCH_LINE", 16)
+    monkeypatch.setattr(A, "_PITCH_ALIGN", 64)
+    monkeypatch.setattr(A, "_PITCH_PAD_DIV", 0)
+    monkeypatch.setattr(A, "_PITCH_PLANS", {})
+
+
+def _padded(b):
+    return "_pbuf" in b.__dict__
+
+
+def _mv(shape, perm):
+    return A._move_plan(shape, perm, 1)
+
+
+def test_pitch_plan_thresholds():
+    # C2: swap((0,),(0,1)) of (2000, 512, 512) float32 -> rows of 2000 at 8192 B
+    pp = A._pitch_plan(_mv((2000, 512, 512), (1, 2, 0)), (2000, 512, 512), 4)
+    assert pp is not None
+    P, rows, oshape, sstr, dstr = pp
+    assert P == 2048 and rows == 512 * 512 and oshape == [512, 512, 2000]
+    assert sstr == [512, 1, 512 * 512] and dstr == [512 * 2048, 2048, 1]
+    # float64 rows of 16000 B are whole lines already
+    assert A._pitch_plan(_mv((2000, 512, 512), (1, 2, 0)), (2000, 512, 512), 8) is None
+    # the last axis stays put: a row copy, rows written whole
+    assert A._pitch_plan(_mv((4096, 256, 250), (1, 0, 2)), (4096, 256, 250), 4) is None
+    # short rows, and rows whose padding would exceed 1/32
+    assert A._pitch_plan(_mv((1000, 64), (1, 0)), (1000, 64), 2) is None
+    assert A._pitch_plan(_mv((1100, 64), (1, 0)), (1100, 64), 4) is None   # 4400 -> 5120 B
+    assert A._pitch_plan(_mv((8100, 64), (1, 0)), (8100, 64), 4) is not None  # 32400 -> 33792 B
+    # one row: nothing to align
+    assert A._pitch_plan(_mv((2000, 1), (1, 0)), (2000, 1), 4) is None
+
+
+CASES = [((41, 3, 5), (0,), (0, 1), np.float32),
+         ((37, 4, 6), (0,), (0, 1), np.float64),
+         ((9, 3, 7), (0,), (1,), np.int16),
+         ((21, 2, 3, 5), (0, 1), (1,), np.uint8),
+         ((13, 6), (0,), (0,), np.int32),
+         ((11, 5, 4), (0,), (0, 1), np.uint16)]
+
+
+def _data(shape, dtype, seed=0):
+    rng = np.random.default_rng(seed)
+    if np.dtype(dtype).kind == "f":
+        return (3 + rng.standard_normal(shape)).astype(dtype)
+    return rng.integers(0, 60, size=shape).astype(dtype)
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_padded_statistics(bctx, small_pitch, case):
+    shape, kax, vax, dtype = CASES[case]
+    x = _data(shape, dtype, case)
+    b = bolt.array(x, bctx, axis=tuple(range(len(kax))))
+    s = b.swap(kax, vax)
+    assert _padded(s), "the small-pitch settings pad this swap"
+    want = np.ascontiguousarray(bolt.array(x, bctx, axis=tuple(range(len(kax)))).swap(kax, vax).toarray())
+    last = s.ndim - 1
+    for name in ("mean", "var", "std"):
+        got = getattr(s, name)(axis=last)
+        truth = getattr(want.astype(np.float64), name)(axis=last)
+        assert np.allclose(got, truth, rtol=1e-5, atol=1e-6), name
+    for name, uf in (("sum", np.add), ("min", np.minimum), ("max", np.maximum)):
+        got = np.asarray(getattr(s, name)(axis=last))
+        w = np.asarray(uf.reduce(want, axis=last, dtype=want.dtype))
+        assert got.dtype == w.dtype and got.shape == w.shape, name
+        if name != "sum" or w.dtype.kind in "iub":
+            assert got.tobytes() == w.tobytes(), name
+        else:
+            assert G.reduce_close(got, w, want, "add", (last,)), name
+    assert _padded(s), "last-axis statistics read the padded rows in place"
+    # a statistic over other axes compacts, then the dense path answers
+    assert np.allclose(s.mean(axis=0), want.astype(np.float64).mean(axis=0), rtol=1e-5, atol=1e-6)
+    assert not _padded(s)
+    assert s.toarray().tobytes() == want.tobytes()
+
+
+def _consumers(kax, vax):
+    """(name, f(swapped bolt array) -> ndarray)."""
+    back = (tuple(range(len(vax))), tuple(range(len(kax))))
+    return [
+        ("toarray", lambda s: s.toarray()),
+        ("T", lambda s: s.T.toarray()),
+        ("swap back", lambda s: s.swap(*back).toarray()),
+        ("chunk", lambda s: s.chunk((2,) * len(s.values.shape)).unchunk().toarray()),
+        ("map", lambda s: s.map(lambda v: v * 2, axis=tuple(range(s.split))).toarray()),
+        ("getitem", lambda s: s[1:, ::2].toarray()),
+        ("astype", lambda s: s.astype(np.float64).toarray()),
+        ("concatenate", lambda s: s.concatenate(np.ascontiguousarray(s.toarray()), axis=0).toarray()),
+        ("values.reshape", lambda s: s.values.reshape((int(np.prod(s.values.shape)),)).toarray()),
+        ("first", lambda s: np.asarray(s.first())),
+        ("sum all", lambda s: np.asarray(s.sum(axis=None))),
+        ("var axis 0", lambda s: np.asarray(s.var(axis=0))),
+    ]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_padded_consumers(bctx, small_pitch, monkeypatch, case):
+    """Every other use of a padded result equals the same use of the dense one."""
+    shape, kax, vax, dtype = CASES[case]
+    x = _data(shape, dtype, 100 + case)
+    axis = tuple(range(len(kax)))
+    for name, f in _consumers(kax, vax):
+        s = bolt.array(x, bctx, axis=axis).swap(kax, vax)
+        assert _padded(s)
+        got = f(s)
+        monkeypatch.setattr(A, "ROW_PITCH", False)
+        d = bolt.array(x, bctx, axis=axis).swap(kax, vax)
+        assert not _padded(d)
+        want = f(d)
+        monkeypatch.setattr(A, "ROW_PITCH", True)
+        got, want = np.asarray(got), np.asarray(want)
+        assert got.shape == want.shape and got.dtype == want.dtype, name
+        assert got.tobytes() == want.tobytes(), name
+
+
+def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
+    monkeypatch.setattr(A, "ROW_PITCH", False)
+    x = _data((41, 3, 5), np.float32)
+    s = bolt.array(x, bctx).swap((0,), (0, 1))
+    assert not _padded(s)
+    assert s.toarray().tobytes() == np.ascontiguousarray(x.transpose(1, 2, 0)).tobytes()
+
+
+NSEEDS = 60
+
+
+@pytest.fixture
+def padded_inputs(small_pitch, monkeypatch):
+    """bolt.array builds its arrays as padded transposition results: the
+    records of x.moveaxis(-1, 0), transposed back (same shape, split and
+    values as x), so every operation of a suite starts from padded rows."""
+    orig = bolt.array
+
+    def array(x, context=None, axis=(0,), **kw):
+        x = np.asarray(x)
+        if x.ndim < 2 or context is None or kw:
+            return orig(x, context, axis=axis, **kw)
+        y = np.ascontiguousarray(np.moveaxis(x, -1, 0))
+        b = orig(y, context, axis=axis)
+        return b.transpose(*(tuple(range(1, x.ndim)) + (0,)))
+    monkeypatch.setattr(bolt, "array", array)
+
+
+@pytest.mark.parametrize("seed", range(NSEEDS))
+def test_oracle_fuzz_padded(bctx, padded_inputs, seed):
+    from test_fuzz_oracle import check_case
+    check_case(bctx, seed)
+
+
+@pytest.mark.parametrize("seed", range(NSEEDS))
+def test_api_fuzz_padded(bctx, padded_inputs, seed):
+    from test_api_fuzz import test_api_fuzz
+    test_api_fuzz(bctx, seed)
+
+
+@pytest.mark.parametrize("seed", range(NSEEDS))
+def test_getitem_fuzz_padded(bctx, padded_inputs, seed):
+    from test_getitem_fuzz import test_getitem_fuzz
+    test_getitem_fuzz(bctx, seed)
+
+
+@pytest.mark.parametrize("seed", range(NSEEDS))
+def test_chunk_fuzz_padded(bctx, padded_inputs, seed):
+    from test_chunk_fuzz import test_chunk_fuzz
+    test_chunk_fuzz(bctx, seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.float16, np.int32, np.uint16, np.uint8, np.int64])
+def test_gpu_reduce_rows_abi(gpu_ctx, dtype):
+    """bm_reduce_rows through the C-ABI against bm_reduce on the compacted rows
+    (identical bytes: the same plan over the same values) and numpy."""
+    import torch
+    from bolt_amd.mi355x import _lib
+    from bolt_amd.mi355x._ops import backend_for, dtype_code
+    from bolt_amd.mi355x.transfer import to_device
+    be = backend_for(torch.device("cuda:0"))
+    rng = np.random.default_rng(5)
+    for O, R, P in ((3, 2000, 2048), (257, 1000, 1001), (64, 4097, 4160), (5, 1, 3), (1000, 60, 64)):
+        x = (rng.standard_normal((O, P)) * 7 + 20).astype(dtype) if np.dtype(dtype).kind == "f" else \
+            rng.integers(0, 90, size=(O, P)).astype(dtype)
+        padded = to_device(np.ascontiguousarray(x).reshape(-1).view(np.uint8), torch.device("cuda:0"))
+        dense = to_device(np.ascontiguousarray(x[:, :R]).reshape(-1).view(np.uint8), torch.device("cuda:0"))
+        stats = [_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN]
+        if np.dtype(dtype).kind == "f" or np.dtype(dtype).itemsize <= 4:
+            stats += [_lib.STAT_MEAN, _lib.STAT_VAR, _lib.STAT_STD]
+        for stat in stats:
+            keep = stat in (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN)
+            odt = np.dtype(dtype) if keep else np.dtype(np.float64)
+            a = torch.empty(O * odt.itemsize, dtype=torch.uint8, device="cuda:0")
+            c = torch.empty_like(a)
+            code, ocode = dtype_code(np.dtype(dtype)), dtype_code(odt)
+            be.reduce_rows(stat, padded, code, O, R, P, a, ocode)
+            be.reduce(stat, dense, code, O, R, 1, c, ocode)
+            torch.cuda.synchronize()
+            assert a.cpu().numpy().tobytes() == c.cpu().numpy().tobytes(), (O, R, P, stat)
+            if stat == _lib.STAT_MAX:
+                assert a.cpu().numpy().view(odt).tobytes() == x[:, :R].max(axis=1).tobytes()
+    with pytest.raises(_lib.BoltDeviceError, match="row_pitch"):
+        be.reduce_rows(_lib.STAT_SUM, padded, dtype_code(np.dtype(dtype)), 4, 10, 9, a, dtype_code(np.dtype(dtype)))

@@ -49,5 +49,6 @@ for _ in range(reps):
         step()
     torch.cuda.synchronize()
     ms.append((time.perf_counter() - t0) / steps * 1e3)
-print("%s ms/step median %.4f  min %.4f  all %s" % (os.path.basename(tree.rstrip("/")) or tree, statistics.median(ms),
-                                                    min(ms), " ".join("%.4f" % m for m in ms)), flush=True)
+tag = (os.path.basename(tree.rstrip("/")) or tree) + " pitch=" + os.environ.get("BOLT_AMD_ROW_PITCH", "1")
+print("%s ms/step median %.4f  min %.4f  all %s" % (tag, statistics.median(ms), min(ms),
+                                                    " ".join("%.4f" % m for m in ms)), flush=True)
