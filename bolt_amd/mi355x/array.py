@@ -119,9 +119,10 @@ def _move_plan(shape, perm, split):
 # (bm_reduce_rows); any other use compacts the rows once (_compact).
 ROW_PITCH = os.environ.get("BOLT_AMD_ROW_PITCH", "1") != "0"
 _PITCH_MIN_ROW = 4096            # bytes: shorter rows are not padded
-_PITCH_ALIGN = 1024              # bytes: padded rows start on this boundary
+_PITCH_ALIGN = int(os.environ.get("BOLT_AMD_PITCH_ALIGN", 1024))  # bytes: padded rows start on this boundary
+_PITCH_SKEW = int(os.environ.get("BOLT_AMD_PITCH_SKEW", 0))       # bytes added to the aligned pitch (A/B knob)
 _PITCH_LINE = 128                # bytes: rows of a multiple of this stay dense
-_PITCH_PAD_DIV = 32              # at most 1/32 of a row is padding
+_PITCH_PAD_DIV = int(os.environ.get("BOLT_AMD_PITCH_PAD_DIV", 32))  # at most 1/32 of a row is padding
 _PITCH_MAX_BYTES = 16 << 30      # larger results stay dense (compaction needs a second copy)
 _PITCH_PLANS = {}  # (_move_plan, itemsize) -> None | pitched copy plan
 
@@ -138,7 +139,7 @@ def _pitch_plan(mv, shape, es):
     rb = R * es
     if rb < _PITCH_MIN_ROW or rb % _PITCH_LINE == 0:
         return None
-    pb = -(-rb // _PITCH_ALIGN) * _PITCH_ALIGN
+    pb = -(-rb // _PITCH_ALIGN) * _PITCH_ALIGN + _PITCH_SKEW
     if (pb - rb) * _PITCH_PAD_DIV > rb or pb % es:
         return None
     P = pb // es

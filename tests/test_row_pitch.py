@@ -218,7 +218,14 @@ def test_gpu_reduce_rows_abi(gpu_ctx, dtype):
             be.reduce_rows(stat, padded, code, O, R, P, a, ocode)
             be.reduce(stat, dense, code, O, R, 1, c, ocode)
             torch.cuda.synchronize()
-            assert a.cpu().numpy().tobytes() == c.cpu().numpy().tobytes(), (O, R, P, stat)
+            ga, gc = a.cpu().numpy().view(odt), c.cpu().numpy().view(odt)
+            if P % (16 // np.dtype(dtype).itemsize) == 0 or stat in (_lib.STAT_MAX, _lib.STAT_MIN) \
+                    or (stat == _lib.STAT_SUM and odt.kind in "iu"):
+                # the same plan (vector width) as the dense rows: identical bytes
+                assert ga.tobytes() == gc.tobytes(), (O, R, P, stat)
+            else:
+                # an odd pitch reads element-wise: another summation order
+                assert np.allclose(ga, gc, rtol=2e-3 if odt == np.float16 else 1e-5), (O, R, P, stat)
             if stat == _lib.STAT_MAX:
                 assert a.cpu().numpy().view(odt).tobytes() == x[:, :R].max(axis=1).tobytes()
     with pytest.raises(_lib.BoltDeviceError, match="row_pitch"):
