@@ -1160,7 +1160,7 @@ def make_event(dev):
 
 
 LAUNCHES = ("permute", "copy_strided", "gather_rows", "record_gather", "record_scatter", "record_runs", "reduce",
-            "reduce_state", "reduce_combine")
+            "reduce_rows", "reduce_state", "reduce_combine")
 
 
 class KernelClock(object):
@@ -1495,7 +1495,8 @@ def main():
         # hipEvents bracketing the permute kernel's own launch, on the stream it
         # runs on (one permute launch per swap on one GPU; the pipelined
         # multi-GPU swap launches more and draws extra pairs)
-        clock = KernelClock(be, dev, ("permute",), pool=steps)
+        # permute; copy_strided when the result is stored at a padded row pitch
+        clock = KernelClock(be, dev, ("permute", "copy_strided"), pool=steps)
         swap_ev = {} if world > 1 else None
         if world > 1:
             bdist.PROFILE = {}  # hipEvent pairs around pack / all_to_all / unpack
@@ -1545,7 +1546,7 @@ def main():
             "legend": LEGEND,
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("bm_permute (%s)" % ops[0][0]) if world == 1 else "swap exchange per rank",
+                "kernel": ("bm_permute / bm_copy_strided (%s)" % ops[0][0]) if world == 1 else "swap exchange per rank",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
@@ -1595,7 +1596,8 @@ def main():
         if stat_ops and world == 1:
             # the reduction kernels' own hipEvents, in K more steps (kept out of the
             # timed region above: every extra event adds a few us to the step)
-            clock = KernelClock(be, dev, ("reduce", "reduce_state", "reduce_combine"), pool=steps * len(stat_ops))
+            clock = KernelClock(be, dev, ("reduce", "reduce_rows", "reduce_state", "reduce_combine"),
+                                pool=steps * len(stat_ops))
             try:
                 timed_steps(ops, steps, clock=clock, op_filter=stat_ops)
             finally:
