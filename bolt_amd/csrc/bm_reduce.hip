@@ -654,6 +654,20 @@ __global__ void __launch_bounds__(kThreads)
 }
 
 // ------------------------------------------------------------------ rows --
+// Round-robin dispatch puts block b on XCD b % 8: give XCD x the x-th
+// contiguous eighth of the rows, so the 128-B lines two neighbouring rows
+// share are fetched into one L2 instead of two (runs of 16 / 128 / 1024
+// blocks per XCD in turn: no better, padded rows 5% worse at 16,
+// profiles/r05w_xcd_runs.txt)
+__device__ __forceinline__ uint64_t rows_block() {
+  uint64_t bid = blockIdx.x;
+  if (BM_RED_XCD) {
+    const uint64_t g8 = gridDim.x / 8 * 8;
+    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
+  }
+  return bid;
+}
+
 struct RowsDesc {
   int64_t O, R;
   int64_t P;       // elements between row starts (R, or a padded row pitch >= R)
@@ -667,14 +681,7 @@ template <typename T, int VEC, int MODE>
 __global__ void __launch_bounds__(kThreads)
     k_red_rows(const T *__restrict__ src, RowsDesc d, Sink sk) {
   const int lane = threadIdx.x & 63;
-  uint64_t bid = blockIdx.x;
-  if (BM_RED_XCD) {
-    // round-robin dispatch puts block b on XCD b % 8: give XCD x the x-th
-    // contiguous eighth of the rows, so the 128-B lines two neighbouring
-    // rows share are fetched into one L2 instead of two
-    const uint64_t g8 = gridDim.x / 8 * 8;
-    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
-  }
+  const uint64_t bid = rows_block();
   const int64_t item = d.item0 + (int64_t)bid * (kThreads / 64) + (threadIdx.x >> 6);
   if (item >= d.nitems) return;  // whole wave exits; no block barrier below
   const uint64_t o = fd_div((uint64_t)item, d.nchunks);
@@ -940,11 +947,7 @@ template <typename T, int VEC>
 __global__ void __launch_bounds__(kThreads)
     k_red_rows_int(const T *__restrict__ src, RowsDesc d, Sink sk) {
   const int lane = threadIdx.x & 63;
-  uint64_t bid = blockIdx.x;
-  if (BM_RED_XCD) {
-    const uint64_t g8 = gridDim.x / 8 * 8;
-    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
-  }
+  const uint64_t bid = rows_block();
   const int64_t item = d.item0 + (int64_t)bid * (kThreads / 64) + (threadIdx.x >> 6);
   if (item >= d.nitems) return;  // whole wave exits
   const uint64_t o = fd_div((uint64_t)item, d.nchunks);
