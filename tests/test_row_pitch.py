@@ -11,6 +11,8 @@ small arrays of the seeded suites take the padded path too; the oracle suites
 test_chunk_fuzz.py) then run again over padded swap results.  Runs on the CPU
 test executor and (marker ``gpu``) on the HIP kernels.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -147,6 +149,8 @@ def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
 
 
 NSEEDS = 60
+# a soak run takes other seeds: BOLT_AMD_PITCH_SEEDS=start:stop (default 0:NSEEDS)
+_SEEDS = range(*[int(v) for v in os.environ.get("BOLT_AMD_PITCH_SEEDS", "0:%d" % NSEEDS).split(":")])
 
 
 @pytest.fixture
@@ -166,25 +170,25 @@ def padded_inputs(small_pitch, monkeypatch):
     monkeypatch.setattr(bolt, "array", array)
 
 
-@pytest.mark.parametrize("seed", range(NSEEDS))
+@pytest.mark.parametrize("seed", _SEEDS)
 def test_oracle_fuzz_padded(bctx, padded_inputs, seed):
     from test_fuzz_oracle import check_case
     check_case(bctx, seed)
 
 
-@pytest.mark.parametrize("seed", range(NSEEDS))
+@pytest.mark.parametrize("seed", _SEEDS)
 def test_api_fuzz_padded(bctx, padded_inputs, seed):
     from test_api_fuzz import test_api_fuzz
     test_api_fuzz(bctx, seed)
 
 
-@pytest.mark.parametrize("seed", range(NSEEDS))
+@pytest.mark.parametrize("seed", _SEEDS)
 def test_getitem_fuzz_padded(bctx, padded_inputs, seed):
     from test_getitem_fuzz import test_getitem_fuzz
     test_getitem_fuzz(bctx, seed)
 
 
-@pytest.mark.parametrize("seed", range(NSEEDS))
+@pytest.mark.parametrize("seed", _SEEDS)
 def test_chunk_fuzz_padded(bctx, padded_inputs, seed):
     from test_chunk_fuzz import test_chunk_fuzz
     test_chunk_fuzz(bctx, seed)
