@@ -149,11 +149,18 @@ def _pitch_plan(mv, shape, es):
     sstr = [1] * len(shape)
     for k in range(len(shape) - 2, -1, -1):
         sstr[k] = sstr[k + 1] * shape[k + 1]
-    dstr = [1] * nd
-    dstr[nd - 2] = P
-    for k in range(nd - 3, -1, -1):
-        dstr[k] = dstr[k + 1] * new_shape[k + 1]
-    return P, rows, list(new_shape), [sstr[p] for p in perm], dstr
+    return P, rows, list(new_shape), [sstr[p] for p in perm], _padded_strides(new_shape, P)
+
+
+def _padded_strides(shape, P):
+    """C-order element strides of ``shape`` with rows (the last axis) P elements apart."""
+    nd = len(shape)
+    st = [1] * nd
+    if nd >= 2:
+        st[nd - 2] = P
+        for k in range(nd - 3, -1, -1):
+            st[k] = st[k + 1] * shape[k + 1]
+    return st
 
 
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
@@ -389,17 +396,29 @@ class BoltArrayMI355X(BoltArray):
                 if len(_PITCH_PLANS) > 4096:
                     _PITCH_PLANS.clear()
                 _PITCH_PLANS[key] = pp
-            src = self._data
+            d = self.__dict__
+            if "_pbuf" in d:
+                # a padded source is read in place: its strides, permuted
+                src, pstr = d["_pbuf"], _padded_strides(self._shape, d["_pitch"])
+                sstr = [pstr[p] for p in perm]
+            else:
+                src, sstr = self._data, None
+            be = backend_for(src.device)
             if pp is not None:
-                P, rows, oshape, sstr, dstr = pp
+                P, rows, oshape, psstr, dstr = pp
                 pbuf = _empty(rows * P * es, src.device)
-                backend_for(src.device).copy_strided(src, 0, pbuf, 0, oshape, sstr, dstr, es)
+                be.copy_strided(src, 0, pbuf, 0, oshape, psstr if sstr is None else sstr, dstr, es)
                 new = self._derive(None, new_shape, split)
-                d = new.__dict__
-                del d["_data"]
-                d["_pbuf"], d["_pitch"] = pbuf, P
+                nd = new.__dict__
+                del nd["_data"]
+                nd["_pbuf"], nd["_pitch"] = pbuf, P
                 return new
-            data = permute_sharded(self._ctx, backend_for(src.device), src, self._shape, perm, es)
+            if sstr is None:
+                data = permute_sharded(self._ctx, be, src, self._shape, perm, es)
+            else:
+                n = int(np.prod(new_shape, dtype=np.int64))
+                data = _empty(n * es, src.device)
+                be.copy_strided(src, 0, data, 0, list(new_shape), sstr, _padded_strides(new_shape, new_shape[-1]), es)
         else:
             data = permute_sharded(self._ctx, backend_for(self._data.device), self._data, self._shape, perm,
                                    self._dtype.itemsize)
@@ -874,14 +893,21 @@ class BoltArrayMI355X(BoltArray):
             be.reduce_rows(stat, pbuf, code, O, R, self._pitch, out, ocode)
             return to_host(out, out_dtype, out_shape), out_dtype
         be = self._backend
-        dev = self._data.device
+        dev = self._device
         es = self._dtype.itemsize
-        src = self._data
         if perm is not None:
-            tmp = _empty(src.numel(), dev)
-            if src.numel():
-                be.permute(src, lshape, perm, es, tmp)
+            # the reduced axes first (_align's swap): a padded array is read in place
+            tmp = _empty(nloc * es, dev)
+            if pbuf is not None:
+                pstr = _padded_strides(lshape, self._pitch)
+                pshape = [lshape[p] for p in perm]
+                be.copy_strided(pbuf, 0, tmp, 0, pshape, [pstr[p] for p in perm],
+                                _padded_strides(pshape, pshape[-1]), es)
+            elif nloc:
+                be.permute(self._data, lshape, perm, es, tmp)
             src = tmp
+        else:
+            src = self._data
 
         if ctx.world_size == 1 or 0 not in axset:
             # every output lives on this rank (or this rank's slab of them)

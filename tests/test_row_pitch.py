@@ -95,6 +95,11 @@ def test_padded_statistics(bctx, small_pitch, case):
         else:
             assert G.reduce_close(got, w, want, "add", (last,)), name
     assert _padded(s), "last-axis statistics read the padded rows in place"
+    if s.ndim >= 3:
+        # axes that are not one block: permuted to the front straight from the padded rows
+        got = s.var(axis=(0, last))
+        assert np.allclose(got, want.astype(np.float64).var(axis=(0, last)), rtol=1e-5, atol=1e-6)
+        assert _padded(s)
     # a statistic over other axes compacts, then the dense path answers
     assert np.allclose(s.mean(axis=0), want.astype(np.float64).mean(axis=0), rtol=1e-5, atol=1e-6)
     assert not _padded(s)
@@ -117,6 +122,7 @@ def _consumers(kax, vax):
         ("first", lambda s: np.asarray(s.first())),
         ("sum all", lambda s: np.asarray(s.sum(axis=None))),
         ("var axis 0", lambda s: np.asarray(s.var(axis=0))),
+        ("max first and last", lambda s: np.asarray(s.max(axis=(0, s.ndim - 1)))),
     ]
 
 
