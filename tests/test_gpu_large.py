@@ -82,10 +82,17 @@ def test_swap_full_size(gpu_ctx, cfg):
     s = b.swap(kax, vax)
     from bolt_amd.mi355x.plan import swap_perm
     perm, nsplit = swap_perm(len(shape), split, kax, vax)
+    inv = list(np.argsort(perm))
+    if name == "C2":
+        # padded rows (8192-B pitch), transposed back straight from the padding
+        assert "_pbuf" in s.__dict__
+        back = s.transpose(inv)
+        assert "_pbuf" in s.__dict__
+        assert torch.equal(back._data, b._data)
+        del back
     assert s.shape == tuple(shape[p] for p in perm) and s.split == nsplit
     _full_check(raw, shape, dtype, s, perm)
     # undo the swap with the inverse permutation: bit-exact identity
-    inv = list(np.argsort(perm))
     back = s.transpose(inv)
     assert torch.equal(back._data, b._data)
     del s, back
