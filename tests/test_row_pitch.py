@@ -2,7 +2,8 @@
 
 A swap / transpose whose output rows are not a whole number of 128-B lines is
 stored with padded rows; statistics over the last axis read them in place
-(bm_reduce_rows) and every other use compacts them first.  Results must be
+(bm_reduce_rows), swaps / transposes and permuted reductions read them with
+the pitch as the source row stride, and every other use compacts them first.  Results must be
 the dense layout's: statistics against numpy (float64 truth within
 golden_cases.reduce_close for float sums, exact otherwise), data movement
 bit-exact.  The size thresholds are lowered here (``small_pitch``) so that the
