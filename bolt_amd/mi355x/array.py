@@ -113,10 +113,14 @@ def _move_plan(shape, perm, split):
 # 256-B tile segments; rows whose length is not a multiple of the 128-B line
 # start mid-line every other row (C2's 2000 float32 = 8000 B), so neighbouring
 # tiles write halves of the same lines.  Such a result is stored with its rows
-# padded to a 1-KiB multiple (8192 B): the C2 transpose 0.722 -> 0.674 ms and
-# its time-axis statistics 0.312 -> 0.297 ms (profiles/r05r_tpitch.log).
-# Statistics over the last axis read the padded rows in place
-# (bm_reduce_rows); any other use compacts the rows once (_compact).
+# padded to a 1-KiB multiple (8192 B): the C2 transpose 0.729 -> 0.675 ms, its
+# time-axis statistics 0.298 -> 0.301-0.305 ms, the step -2.8%
+# (profiles/r05s_pitch_prof.txt, r05s_pitch_ab.log; pitch sweep
+# r05t_pitch_sweep.txt).  Statistics over the last axis read the padded rows
+# in place (bm_reduce_rows), swaps / transposes and permuted reductions read
+# them with the pitch as the source row stride; any other use compacts the
+# rows once (_compact).  BOLT_AMD_ROW_PITCH=0 turns padding off; the
+# ALIGN / SKEW / PAD_DIV variables are the sweep's knobs (tools/pitch_sweep.sh).
 ROW_PITCH = os.environ.get("BOLT_AMD_ROW_PITCH", "1") != "0"
 _PITCH_MIN_ROW = 4096            # bytes: shorter rows are not padded
 _PITCH_ALIGN = int(os.environ.get("BOLT_AMD_PITCH_ALIGN", 1024))  # bytes: padded rows start on this boundary
