@@ -658,12 +658,21 @@ __global__ void __launch_bounds__(kThreads)
 // contiguous eighth of the rows, so the 128-B lines two neighbouring rows
 // share are fetched into one L2 instead of two (runs of 16 / 128 / 1024
 // blocks per XCD in turn: no better, padded rows 5% worse at 16,
-// profiles/r05w_xcd_runs.txt)
+// profiles/r05w_xcd_runs.txt).  XCD x starts its eighth x * SKEW blocks in
+// and wraps, so the eight XCDs are never a power-of-two distance apart: on
+// C2's padded rows (8192-B pitch, eighths 256 MiB apart) mean / std
+// -1.2% / -1.0% over 3 alternating rounds (profiles/r05zd_xcd_skew.txt)
+#ifndef BM_RED_XCD_SKEW
+#define BM_RED_XCD_SKEW 37
+#endif
 __device__ __forceinline__ uint64_t rows_block() {
   uint64_t bid = blockIdx.x;
   if (BM_RED_XCD) {
     const uint64_t g8 = gridDim.x / 8 * 8;
-    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
+    if (bid < g8) {
+      const uint64_t E = g8 / 8;
+      bid = (bid % 8) * E + (BM_RED_XCD_SKEW ? (bid / 8 + (bid % 8) * BM_RED_XCD_SKEW) % E : bid / 8);
+    }
   }
   return bid;
 }
