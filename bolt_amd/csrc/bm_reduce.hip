@@ -423,6 +423,9 @@ __device__ __forceinline__ void emit(const Sink &sk, int64_t e, double n, double
 // blockIdx.x, with the blocks the hardware deals to one XCD (every 8th)
 // remapped to consecutive indices when BM_COLS_XCD (a bijection of the grid):
 // each XCD then reads one contiguous range of every row
+// (the rows kernel's rotated start, rows_block, does not help the columns:
+// -0.1...-0.6% on the 64 GiB target / C4 / C2 column statistics,
+// profiles/r05zf_ab_colskew.log)
 __device__ __forceinline__ uint64_t xcd_block() {
   uint64_t bid = blockIdx.x;
   if (BM_COLS_XCD) {
