@@ -637,8 +637,19 @@ class BoltArrayMI355X(BoltArray):
     def first(self):
         """The first record's value, on the host (array.py:117-123)."""
         from bolt_amd.mi355x.dist import all_gather_bytes
-        rb = int(np.prod(self._shape[self._split:], dtype=np.int64)) * self._dtype.itemsize
-        buf = self._data[:rb]
+        es = self._dtype.itemsize
+        rec = int(np.prod(self._shape[self._split:], dtype=np.int64))
+        rb = rec * es
+        d = self.__dict__
+        if "_pbuf" in d and rec > self._shape[-1]:
+            # padded rows: gather the first record's rows, no compaction
+            R = self._shape[-1]
+            buf = _empty(rb, d["_pbuf"].device)
+            self._backend.copy_strided(d["_pbuf"], 0, buf, 0, [rec // R, R], [d["_pitch"], 1], [R, 1], es)
+        elif "_pbuf" in d:
+            buf = d["_pbuf"][:rb]  # within the first row
+        else:
+            buf = self._data[:rb]
         if self._ctx.world_size > 1:
             lo, hi = self._ctx.bounds(self._shape[0])[0]
             sizes = [rb if r == 0 else 0 for r in range(self._ctx.world_size)]

@@ -20,6 +20,7 @@ of an all-key array (which the reference cannot do) must be numpy's, and
 filter is compared in key order (the reference's sort=True).
 
     PYTHONDONTWRITEBYTECODE=1 python tools/reference_diff_fuzz.py 0 2000
+    BOLT_AMD_DIFF_PADDED=1 ... (the same with padded rows for small arrays)
 """
 import os
 import sys
@@ -46,6 +47,21 @@ DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16, np.uint16]
 # reference's swaps misbehave (docs/HISTORY.md §4 item 6): a survey, not a gate
 MIN_EXTENT = int(os.environ.get("BOLT_AMD_DIFF_MIN_EXTENT", "2"))
 CATALOGUE = os.environ.get("BOLT_AMD_DIFF_CATALOGUE") == "1"  # list every difference, by message
+if os.environ.get("BOLT_AMD_DIFF_PADDED") == "1":
+    # every transposed result whose rows are not a multiple of 16 B is stored
+    # with padded rows (tests/test_row_pitch.py's small_pitch settings)
+    import bolt_amd.mi355x.array as _A
+    _A._PITCH_MIN_ROW, _A._PITCH_LINE, _A._PITCH_ALIGN, _A._PITCH_PAD_DIV = 1, 16, 64, 0
+    PADDED = [0]
+    _plan = _A._pitch_plan
+
+    def _counted(*a):
+        r = _plan(*a)
+        PADDED[0] += r is not None
+        return r
+    _A._pitch_plan = _counted
+else:
+    PADDED = None
 
 
 class Refused(Exception):
@@ -365,6 +381,8 @@ def main(lo, hi):
         bad = bad[:3]
     print("seeds %d..%d: %d failed, operations compared %s, %.0f s"
           % (lo, hi - 1, len(bad), dict(sorted(counts.items())), time.time() - t0))
+    if PADDED is not None:
+        print("padded rows: %d distinct padded move plans" % PADDED[0])
     for seed, tb in bad:
         print("seed %d:\n%s" % (seed, tb))
     return 1 if bad else 0
