@@ -661,7 +661,15 @@ class BoltArrayMI355X(BoltArray):
         from bolt_amd.mi355x import functional as F
         lshape = self._local_shape
         nrec = int(np.prod(lshape[:self._split], dtype=np.int64))
-        return F.view(self._data, (nrec,) + tuple(self._shape[self._split:]), self._dtype)
+        vshape = tuple(self._shape[self._split:])
+        d = self.__dict__
+        if "_pbuf" in d and vshape and int(np.prod(vshape[:-1], dtype=np.int64)) == 1:
+            # padded rows, one row per record: each record is still contiguous
+            # (only the records are P elements apart), so the functions that
+            # see them cannot tell; no compaction
+            rows = F.view(d["_pbuf"], (nrec, d["_pitch"]), self._dtype)[:, :vshape[-1]]
+            return rows.view((nrec,) + vshape)
+        return F.view(self._data, (nrec,) + vshape, self._dtype)
 
     def map(self, func, axis=(0,), value_shape=None, dtype=None, with_keys=False):
         """Apply ``func`` to every record along ``axis`` (array.py:125-191).
@@ -675,7 +683,7 @@ class BoltArrayMI355X(BoltArray):
         from bolt_amd.mi355x import functional as F
         axis = tupleize(axis)
         swapped = self._align(axis)
-        dev = swapped._data.device
+        dev = swapped._device
         func = F.user_fn(func)
         test_func = (lambda x: func((F.KeyTuple((0,) * len(axis)), x))) if with_keys else func
         if value_shape is None or dtype is None:
@@ -728,7 +736,7 @@ class BoltArrayMI355X(BoltArray):
             import torch
             per = int(np.prod(swapped.shape[1:swapped.split], dtype=np.int64))
             sizes = [(hi - lo) * per for lo, hi in ctx.bounds(swapped.shape[0])]
-            mb = torch.from_numpy(mask.astype(np.uint8)).to(swapped._data.device)
+            mb = torch.from_numpy(mask.astype(np.uint8)).to(swapped._device)
             allm = all_gather_bytes(ctx, mb, sizes).cpu().numpy()
             glob = np.nonzero(allm)[0].astype(np.int64)
         else:
@@ -739,7 +747,7 @@ class BoltArrayMI355X(BoltArray):
         rowbytes = int(np.prod(remaining, dtype=np.int64)) * es
         nrec = int(np.prod(swapped.shape[:swapped.split], dtype=np.int64))
         if count == 0:
-            return self._like(_empty(0, swapped._data.device), (0,), 1)
+            return self._like(_empty(0, swapped._device), (0,), 1)
         # records are rows of the flattened key space; ragged per rank
         flat_rows_per_lead = int(np.prod(swapped.shape[1:swapped.split], dtype=np.int64))
         data = gather_units_sharded(ctx, swapped._backend, swapped._data, swapped.shape[0],

@@ -147,6 +147,22 @@ def test_padded_consumers(bctx, small_pitch, monkeypatch, case):
         assert got.tobytes() == want.tobytes(), name
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16, np.float64])
+def test_map_reads_padded_records(bctx, small_pitch, dtype):
+    """One row per record (the time series after C2's swap): map sees the
+    padded rows as the records, without compacting the array (filter's
+    predicate too; its row gather then compacts)."""
+    x = _data((37, 3, 4), dtype, 9)
+    s = bolt.array(x, bctx).swap((0,), (0, 1))
+    assert _padded(s) and s.split == 2
+    want = np.ascontiguousarray(x.transpose(1, 2, 0))
+    got = s.map(lambda v: v * 3 + 1, axis=(0, 1)).toarray()
+    assert got.tobytes() == (want * 3 + 1).astype(got.dtype).tobytes()
+    assert _padded(s), "map over single-row records reads the padded rows"
+    keep = s.filter(lambda v: float(v.double().sum() if hasattr(v, "double") else v.sum()) > 0, axis=(0, 1))
+    assert keep.shape == (12, 37) and keep.toarray().tobytes() == want.reshape(12, 37).tobytes()
+
+
 def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
     monkeypatch.setattr(A, "ROW_PITCH", False)
     x = _data((41, 3, 5), np.float32)

@@ -1,6 +1,7 @@
 """What a padded C2 swap result costs its other users (one GPU): the
-compaction copy (`_compact`), and a transpose back read straight from the
-padded rows against the same transpose of the dense result.  hipEvents on
+compaction copy (`_compact`), a transpose back read straight from the
+padded rows against the same transpose of the dense result, and swap + map
+(records = padded rows) against swap + map on dense rows.  hipEvents on
 the current stream, median of N.
 
     python tools/compact_probe.py [N]
@@ -77,3 +78,29 @@ assert "_pbuf" in s_pad.__dict__
 print("T of the dense result    %.4f ms" % timed(lambda: s_dense.T), flush=True)
 assert torch.equal(s_pad.T._data, s_dense.T._data)
 print("ok: transposes of the padded and dense results identical", flush=True)
+
+
+def map_of(make):
+    def f():
+        make().map(lambda v: v * 2 + 1, axis=(0, 1))
+    return f
+
+
+def padded():
+    return b.swap((0,), (0, 1))
+
+
+def dense():
+    A.ROW_PITCH = False
+    try:
+        return b.swap((0,), (0, 1))
+    finally:
+        A.ROW_PITCH = True
+
+
+print("swap + map, padded rows  %.4f ms" % timed(map_of(padded)), flush=True)
+print("swap + map, dense rows   %.4f ms" % timed(map_of(dense)), flush=True)
+mp = padded().map(lambda v: v * 2 + 1, axis=(0, 1))
+md = dense().map(lambda v: v * 2 + 1, axis=(0, 1))
+assert torch.equal(mp._data, md._data)
+print("ok: maps identical", flush=True)
