@@ -771,7 +771,12 @@ class BoltArrayMI355X(BoltArray):
             starts = [s.start for s in index]
             steps = [s.step for s in index]
             shape = tuple(int(np.ceil((s.stop - s.start) / float(s.step))) for s in index)
-            data = select_sharded(self._ctx, self._backend, self._data, self._shape, starts, steps, shape, es)
+            d = self.__dict__
+            if "_pbuf" in d:  # padded rows: selected in place, no compaction
+                data = select_sharded(self._ctx, self._backend, d["_pbuf"], self._shape, starts, steps, shape, es,
+                                      src_strides=_padded_strides(self._shape, d["_pitch"]))
+            else:
+                data = select_sharded(self._ctx, self._backend, self._data, self._shape, starts, steps, shape, es)
             result = self._like(data, shape, self._split)
         elif kind == 'advanced':
             pts, shape = indexing.advanced_points(index, self._shape, self._split)

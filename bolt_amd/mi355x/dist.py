@@ -461,13 +461,15 @@ def _unpack(backend, pending, out, tstr, es, even=False):
     del send
 
 
-def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es):
+def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es, src_strides=None):
     """This rank's slab of x[start_k :: step_k] (basic slicing) for a sharded x.
 
     Output row i of the leading axis is input row starts[0] + i*steps[0].  On
     one GPU this is a single strided copy; across GPUs each rank packs, for
     every destination, the selected rows it holds (they form one run of
     output rows), one all-to-all moves them, and they land in order.
+    ``src_strides``: element strides of a source that is not C-contiguous (a
+    row-padded array, one GPU only).
     """
     shape = tuple(int(x) for x in shape)
     out_shape = tuple(int(x) for x in out_shape)
@@ -481,6 +483,10 @@ def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es):
     r = ctx.rank
     mlo, mhi = in_b[r]
     sin = contiguous_strides((mhi - mlo,) + shape[1:])
+    if src_strides is not None:
+        if ctx.world_size != 1:
+            raise ValueError("select_sharded: source strides on one GPU only")
+        sin = [int(v) for v in src_strides]
     sstr = [sin[k] * steps[k] for k in range(len(shape))]
     inner_off = sum(starts[k] * sin[k] for k in range(1, len(shape)))
     lo, hi = out_b[r]

@@ -163,6 +163,19 @@ def test_map_reads_padded_records(bctx, small_pitch, dtype):
     assert keep.shape == (12, 37) and keep.toarray().tobytes() == want.reshape(12, 37).tobytes()
 
 
+def test_basic_indexing_reads_padded_rows(bctx, small_pitch):
+    """Slices and ints select straight from the padded rows (no compaction)."""
+    x = _data((41, 3, 5), np.float32, 4)
+    s = bolt.array(x, bctx).swap((0,), (0, 1))
+    want = np.ascontiguousarray(x.transpose(1, 2, 0))
+    for index in ((slice(1, None), slice(None, None, 2)), (0, slice(None), slice(3, 30, 4)), (2, 4, 7),
+                  (slice(2, 0, -1), 1, slice(None, None, 3))):
+        got = s[index]
+        w = want[index]
+        assert np.asarray(got.toarray() if hasattr(got, "toarray") else got).tobytes() == np.asarray(w).tobytes()
+    assert _padded(s)
+
+
 def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
     monkeypatch.setattr(A, "ROW_PITCH", False)
     x = _data((41, 3, 5), np.float32)
