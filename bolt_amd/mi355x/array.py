@@ -920,6 +920,24 @@ class BoltArrayMI355X(BoltArray):
             out = _empty(nout * out_dtype.itemsize, pbuf.device)
             be.reduce_rows(stat, pbuf, code, O, R, self._pitch, out, ocode)
             return to_host(out, out_dtype, out_shape), out_dtype
+        if pbuf is not None and perm is None and I > 1 and I % lshape[-1] == 0 and nloc:
+            # leading / middle axes of a row-padded array: the columns run over
+            # the padded rows as if the last axis were P long; every column is
+            # its own reduction, so the pad columns' (unwritten) values reach
+            # only their own outputs, which are dropped
+            be = backend_for(pbuf.device)
+            Rl, P = lshape[-1], self._pitch
+            Ip = I // Rl * P
+            nb = O * Ip * out_dtype.itemsize
+            host = host_result(be, nb, pbuf.device)
+            if host is not None:
+                be.reduce(stat, pbuf, code, O, R, Ip, host, ocode)
+                full = finish_host_result(host, pbuf.device, out_dtype, (O, I // Rl, P))
+            else:
+                out = _empty(nb, pbuf.device)
+                be.reduce(stat, pbuf, code, O, R, Ip, out, ocode)
+                full = to_host(out, out_dtype, (O, I // Rl, P))
+            return np.ascontiguousarray(full[:, :, :Rl]).reshape(out_shape), out_dtype
         be = self._backend
         dev = self._device
         es = self._dtype.itemsize

@@ -162,7 +162,10 @@ class CpuBackend(object):
 
     def reduce(self, stat, src, code, O, R, I, out, out_code):
         x = _np(src).view(_CODES[code]).reshape(O, R, I)
-        self._finish(stat, code, self._planes(stat, code, x), float(R), out, out_code)
+        # (columns over a row-padded array include the pad's unwritten values;
+        # their outputs are dropped, so their overflows are not reported)
+        with np.errstate(all="ignore"):
+            self._finish(stat, code, self._planes(stat, code, x), float(R), out, out_code)
 
     def reduce_rows(self, stat, src, code, O, R, pitch, out, out_code):
         assert pitch >= R

@@ -101,8 +101,13 @@ def test_padded_statistics(bctx, small_pitch, case):
         got = s.var(axis=(0, last))
         assert np.allclose(got, want.astype(np.float64).var(axis=(0, last)), rtol=1e-5, atol=1e-6)
         assert _padded(s)
-    # a statistic over other axes compacts, then the dense path answers
+    # a statistic over the leading axis: the columns run over the padded rows
     assert np.allclose(s.mean(axis=0), want.astype(np.float64).mean(axis=0), rtol=1e-5, atol=1e-6)
+    m0 = np.asarray(s.max(axis=0))
+    assert m0.tobytes() == np.maximum.reduce(want, axis=0).tobytes()
+    assert _padded(s)
+    # over every axis: compacts, then the dense path answers
+    assert np.allclose(s.mean(), want.astype(np.float64).mean(), rtol=1e-5, atol=1e-6)
     assert not _padded(s)
     assert s.toarray().tobytes() == want.tobytes()
 
