@@ -189,7 +189,13 @@ def test_stats_full_size_c2(gpu_ctx):
     d = b.swap((0,), (0, 1))
     d._compact()
     assert d.mean(axis=2).tobytes() == m.tobytes() and d.std(axis=2).tobytes() == sd.tobytes()
-    del d
+    # the leading axis of the padded result: column kernels over the padded rows
+    v0 = s.var(axis=0)
+    assert "_pbuf" in s.__dict__
+    assert np.allclose(v0, d.var(axis=0), rtol=1e-6, atol=0)  # (another column count: maybe another chunking)
+    ref0 = raw.view(torch.float32).reshape(2000, 512, 512).double().var(dim=1, unbiased=False).t().cpu().numpy()
+    assert v0.shape == (512, 2000) and np.all(np.abs(v0 - ref0) <= 1e-6 * ref0 + np.spacing(np.float32(ref0)))
+    del d, ref0
     x = raw.view(torch.float32).reshape(2000, 512 * 512).double()
     mu = x.mean(0)
     var = ((x - mu) ** 2).mean(0)
