@@ -255,8 +255,11 @@ int bm_reduce(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
  * statcounter.py -- when the swap wrote its rows at a line-aligned pitch
  * (a row of 2000 float32 at 8000 B starts 64 B into a line every other row;
  * padded to 8192 B the transpose and this read both run whole lines).
- * Results identical to bm_reduce on the compacted rows; the same workspace
- * (bm_reduce_workspace_bytes with I = 1 covers every pitch).
+ * Results identical to bm_reduce on the compacted rows when row_pitch keeps
+ * the rows' 16-B vector width (a pitch in whole vectors: every padded layout
+ * the array makes; other pitches read narrower vectors, another summation
+ * order); the same workspace (bm_reduce_workspace_bytes with I = 1 covers
+ * every pitch).
  */
 int bm_reduce_rows(int stat, const void *src, int in_dtype, int64_t O, int64_t R,
                    int64_t row_pitch, void *out, int out_dtype, void *workspace,
