@@ -185,26 +185,34 @@ class ChunkedArrayMI355X(object):
 
     # --------------------------------------------------------- pack/unpack
     @staticmethod
-    def _pack(ctx, backend, dense, shape, split, dtype, plan, padding):
-        """Packed chunk buffer for this rank's records of a dense sharded array."""
+    def _pack(ctx, backend, dense, shape, split, dtype, plan, padding, src_stride=None):
+        """Packed chunk buffer for this rank's records of a dense sharded array
+        (``src_stride``: elements between records when they are not back to
+        back -- the single-row records of a row-padded array)."""
         es = np.dtype(dtype).itemsize
         lshape = local_shape(ctx, shape)
         nrec = int(np.prod(lshape[:split], dtype=np.int64))
         vshape = shape[split:]
         geom = ChunkGeometry(vshape, plan, padding)
         rec = int(np.prod(vshape, dtype=np.int64))
+        stride = rec if src_stride is None else int(src_stride)
         if geom.is_identity():
             # the packed layout is the dense one: the chunked array shares the
             # records' bytes (arrays are never written in place)
-            return dense[:nrec * rec * es]
+            if stride == rec:
+                return dense[:nrec * rec * es]
+            packed = _empty(nrec * rec * es, dense.device)
+            if nrec:
+                backend.copy_strided(dense, 0, packed, 0, [nrec, rec], [stride, 1], [rec, 1], es)
+            return packed
         packed = _empty(nrec * geom.size * es, dense.device)
-        if nrec and _use_record_map(rec, es):
-            backend.record_gather(dense, 0, packed, 0, nrec, rec, geom.size,
+        if nrec and _use_record_map(stride, es):
+            backend.record_gather(dense, 0, packed, 0, nrec, stride, geom.size,
                                   geom.record_map(unpack=False), ("pack",) + geom.key(), es)
         elif nrec:
             for (cshape, dstr, pstr, doff, poff) in geom.copies(unpack=False):
                 backend.copy_strided(dense, doff * es, packed, poff * es, [nrec] + cshape,
-                                     [rec] + dstr, [geom.size] + pstr, es)
+                                     [stride] + dstr, [geom.size] + pstr, es)
         return packed
 
     def _unpack(self):
@@ -251,7 +259,14 @@ class ChunkedArrayMI355X(object):
             vshape = shape[split:]
             plan, pad = getplan(vshape, dtype, size, axis, padding)
             check_plan(plan, pad, vshape)
-        packed = cls._pack(barray._ctx, barray._backend, barray._data, shape, split, dtype, plan, pad)
+        d = barray.__dict__
+        if "_pbuf" in d and split == len(shape) - 1:
+            # a row-padded array whose records are single rows: packed straight
+            # from the padded rows (records P elements apart)
+            packed = cls._pack(barray._ctx, barray._backend, d["_pbuf"], shape, split, dtype, plan, pad,
+                               src_stride=d["_pitch"])
+        else:
+            packed = cls._pack(barray._ctx, barray._backend, barray._data, shape, split, dtype, plan, pad)
         return cls(packed, shape=shape, split=split, dtype=dtype, plan=plan, padding=pad,
                    ordered=barray._ordered, context=barray._ctx)
 

@@ -164,6 +164,10 @@ def test_map_reads_padded_records(bctx, small_pitch, dtype):
     got = s.map(lambda v: v * 3 + 1, axis=(0, 1)).toarray()
     assert got.tobytes() == (want * 3 + 1).astype(got.dtype).tobytes()
     assert _padded(s), "map over single-row records reads the padded rows"
+    for size, pad in (((10,), None), ((10,), (2,)), ((37,), None)):
+        c = s.chunk(size, padding=pad)
+        assert c.unchunk().toarray().tobytes() == want.tobytes(), (size, pad)
+    assert _padded(s), "chunk of single-row records packs from the padded rows"
     keep = s.filter(lambda v: float(v.double().sum() if hasattr(v, "double") else v.sum()) > 0, axis=(0, 1))
     assert keep.shape == (12, 37) and keep.toarray().tobytes() == want.reshape(12, 37).tobytes()
 
