@@ -313,6 +313,14 @@ class BoltArrayMI355X(BoltArray):
         del d["_pbuf"], d["_pitch"]
         return data
 
+    def _derive_padded(self, pbuf, pitch, shape, split):
+        """_derive for records stored with padded rows (see ROW_PITCH)."""
+        new = self._derive(None, shape, split)
+        nd = new.__dict__
+        del nd["_data"]
+        nd["_pbuf"], nd["_pitch"] = pbuf, pitch
+        return new
+
     @property
     def _device(self):
         d = self.__dict__
@@ -412,11 +420,7 @@ class BoltArrayMI355X(BoltArray):
                 P, rows, oshape, psstr, dstr = pp
                 pbuf = _empty(rows * P * es, src.device)
                 be.copy_strided(src, 0, pbuf, 0, oshape, psstr if sstr is None else sstr, dstr, es)
-                new = self._derive(None, new_shape, split)
-                nd = new.__dict__
-                del nd["_data"]
-                nd["_pbuf"], nd["_pitch"] = pbuf, P
-                return new
+                return self._derive_padded(pbuf, P, new_shape, split)
             if sstr is None:
                 data = permute_sharded(self._ctx, be, src, self._shape, perm, es)
             else:
@@ -783,16 +787,44 @@ class BoltArrayMI355X(BoltArray):
             if len(shape) == 0:
                 raise ValueError("0-d index arrays are not supported")
             out_upr = int(np.prod(shape[1:], dtype=np.int64))
-            data = indexing.gather_units_sharded(self._ctx, self._backend, self._data, self._shape[0], es,
-                                                 int(np.prod(self._shape[1:], dtype=np.int64)), pts,
+            d = self.__dict__
+            upr = int(np.prod(self._shape[1:], dtype=np.int64))
+            if "_pbuf" in d:
+                # padded rows: the elements' offsets in the padded layout
+                Rl, P = self._shape[-1], d["_pitch"]
+                src, pts, upr = d["_pbuf"], pts // Rl * P + pts % Rl, upr // Rl * P
+            else:
+                src = self._data
+            data = indexing.gather_units_sharded(self._ctx, self._backend, src, self._shape[0], es, upr, pts,
                                                  shape[0], out_upr)
             result = self._like(data, shape, len(shape))
         else:
             loc, idx = indexing.mixed_take(index, self._shape, self._split)
-            data = indexing.take_sharded(self._ctx, self._backend, self._data, self._shape, es, loc, idx)
             newshape = list(self._shape)
             newshape[loc] = len(idx)
-            taken = self._like(data, tuple(newshape), self._split)
+            d = self.__dict__
+            if "_pbuf" in d:
+                # padded rows (one GPU): taking along the last axis gathers
+                # within the rows (a dense result); along another axis whole
+                # padded rows move and the result keeps the pitch
+                P, nd = d["_pitch"], self.ndim
+                n_outer = int(np.prod(self._shape[:min(loc, nd - 1)], dtype=np.int64))
+                if loc == nd - 1:
+                    data = _empty(n_outer * len(idx) * es, d["_pbuf"].device)
+                    if n_outer and len(idx):
+                        self._backend.gather_rows(d["_pbuf"], 0, data, 0, n_outer, P, es, idx)
+                    taken = self._like(data, tuple(newshape), self._split)
+                else:
+                    row = int(np.prod(self._shape[loc + 1:-1], dtype=np.int64)) * P * es
+                    data = _empty(n_outer * len(idx) * row, d["_pbuf"].device)
+                    if data.numel():
+                        self._backend.gather_rows(d["_pbuf"], 0, data, 0, n_outer, self._shape[loc], row, idx)
+                        taken = self._derive_padded(data, P, tuple(newshape), self._split)
+                    else:
+                        taken = self._like(data, tuple(newshape), self._split)
+            else:
+                data = indexing.take_sharded(self._ctx, self._backend, self._data, self._shape, es, loc, idx)
+                taken = self._like(data, tuple(newshape), self._split)
             rest = list(index)
             rest[loc] = slice(0, None, None)
             full = all(isinstance(r, slice) and r.step in (None, 1) and (r.start or 0) == 0 and
