@@ -754,6 +754,14 @@ class BoltArrayMI355X(BoltArray):
             return self._like(_empty(0, swapped._device), (0,), 1)
         # records are rows of the flattened key space; ragged per rank
         flat_rows_per_lead = int(np.prod(swapped.shape[1:swapped.split], dtype=np.int64))
+        d = swapped.__dict__
+        if "_pbuf" in d and remaining:
+            # padded rows (one GPU): whole padded records move, the result keeps the pitch
+            P = d["_pitch"]
+            prb = rowbytes // (remaining[-1] * es) * P * es
+            data = gather_units_sharded(ctx, swapped._backend, d["_pbuf"], swapped.shape[0],
+                                        prb, flat_rows_per_lead, glob, count, 1)
+            return self._derive_padded(data, P, tuple([count] + remaining), 1)
         data = gather_units_sharded(ctx, swapped._backend, swapped._data, swapped.shape[0],
                                     rowbytes, flat_rows_per_lead, glob, count, 1)
         return self._like(data, tuple([count] + remaining), 1)

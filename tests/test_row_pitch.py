@@ -154,9 +154,8 @@ def test_padded_consumers(bctx, small_pitch, monkeypatch, case):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.uint16, np.float64])
 def test_map_reads_padded_records(bctx, small_pitch, dtype):
-    """One row per record (the time series after C2's swap): map sees the
-    padded rows as the records, without compacting the array (filter's
-    predicate too; its row gather then compacts)."""
+    """One row per record (the time series after C2's swap): map, filter and
+    chunk see the padded rows as the records, without compacting the array."""
     x = _data((37, 3, 4), dtype, 9)
     s = bolt.array(x, bctx).swap((0,), (0, 1))
     assert _padded(s) and s.split == 2
@@ -169,7 +168,8 @@ def test_map_reads_padded_records(bctx, small_pitch, dtype):
         assert c.unchunk().toarray().tobytes() == want.tobytes(), (size, pad)
     assert _padded(s), "chunk of single-row records packs from the padded rows"
     keep = s.filter(lambda v: float(v.double().sum() if hasattr(v, "double") else v.sum()) > 0, axis=(0, 1))
-    assert keep.shape == (12, 37) and keep.toarray().tobytes() == want.reshape(12, 37).tobytes()
+    assert keep.shape == (12, 37) and _padded(keep) and _padded(s), "filter gathers padded records"
+    assert keep.toarray().tobytes() == want.reshape(12, 37).tobytes()
 
 
 def test_indexing_reads_padded_rows(bctx, small_pitch, monkeypatch):
