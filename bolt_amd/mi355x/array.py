@@ -568,11 +568,28 @@ class BoltArrayMI355X(BoltArray):
         if not np.can_cast(self._dtype, dtype, casting):
             raise TypeError("Cannot cast array data from %r to %r according to the rule %r"
                             % (self._dtype, dtype, casting))
+        d = self.__dict__
         if dtype == self._dtype:
+            if "_pbuf" in d:
+                return self._derive_padded(d["_pbuf"].clone(), d["_pitch"], self._shape, self._split)
             return self._like(self._data.clone(), self._shape, self._split)
-        src = F.view(self._data, (self._data.numel() // max(1, self._dtype.itemsize),), self._dtype)
+        src = self._elements()
         out = F.as_bytes(src.to(F.torch_dtype(dtype)))
         return self._like(out, self._shape, self._split, dtype=dtype)
+
+    def _elements(self, shape=None):
+        """This rank's elements, in C order, as a torch view of ``shape``
+        (default: flat -- for a row-padded array (rows, row length), a strided
+        view of the padded rows, so elementwise work reads them in place)."""
+        from bolt_amd.mi355x import functional as F
+        d = self.__dict__
+        if "_pbuf" in d:
+            R = self._shape[-1]
+            rows = int(np.prod(self._local_shape[:-1], dtype=np.int64))
+            v = F.view(d["_pbuf"], (rows, d["_pitch"]), self._dtype)[:, :R]
+            return v if shape is None else v.view(tuple(shape))
+        n = self._data.numel() // max(1, self._dtype.itemsize)
+        return F.view(self._data, (n,) if shape is None else tuple(shape), self._dtype)
 
     def clip(self, min=None, max=None):
         """Clip values below ``min`` / above ``max`` (array.py:932-945), on the device.
@@ -585,7 +602,7 @@ class BoltArrayMI355X(BoltArray):
         import torch
         from bolt_amd.mi355x import functional as F
         rdt = np.zeros(1, self._dtype).clip(min=min, max=max).dtype
-        x = F.view(self._data, self._local_shape, self._dtype)
+        x = self._elements(self._local_shape)
         vs = tuple(self._shape[self._split:])
         wide = {1: torch.int16, 2: torch.int32, 4: torch.int64}
         if rdt != self._dtype:

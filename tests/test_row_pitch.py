@@ -123,6 +123,8 @@ def _consumers(kax, vax):
         ("map", lambda s: s.map(lambda v: v * 2, axis=tuple(range(s.split))).toarray()),
         ("getitem", lambda s: s[1:, ::2].toarray()),
         ("astype", lambda s: s.astype(np.float64).toarray()),
+        ("astype same", lambda s: s.astype(s.dtype).toarray()),
+        ("clip", lambda s: s.clip(2, 40).toarray()),
         ("concatenate", lambda s: s.concatenate(np.ascontiguousarray(s.toarray()), axis=0).toarray()),
         ("values.reshape", lambda s: s.values.reshape((int(np.prod(s.values.shape)),)).toarray()),
         ("first", lambda s: np.asarray(s.first())),
@@ -196,6 +198,18 @@ def test_indexing_reads_padded_rows(bctx, small_pitch, monkeypatch):
             assert out[0] == out[1], index
         else:
             assert out[0].shape == out[1].shape and out[0].tobytes() == out[1].tobytes(), index
+
+
+def test_elementwise_reads_padded_rows(bctx, small_pitch):
+    """astype and clip read the padded rows through a strided view."""
+    x = _data((41, 3, 5), np.int16, 6)
+    s = bolt.array(x, bctx).swap((0,), (0, 1))
+    want = np.ascontiguousarray(x.transpose(1, 2, 0))
+    assert s.astype(np.float32).toarray().tobytes() == want.astype(np.float32).tobytes()
+    assert s.clip(5, 30).toarray().tobytes() == want.clip(5, 30).tobytes()
+    same = s.astype(np.int16)
+    assert _padded(same) and same.toarray().tobytes() == want.tobytes()
+    assert _padded(s)
 
 
 def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
