@@ -111,23 +111,28 @@ def _move_plan(shape, perm, split):
 
 # Row pitch of transposed results.  A transpose writes its destination rows in
 # 256-B tile segments; rows whose length is not a multiple of the 128-B line
-# start mid-line every other row (C2's 2000 float32 = 8000 B), so neighbouring
-# tiles write halves of the same lines.  Such a result is stored with its rows
-# padded to a 1-KiB multiple (8192 B): the C2 transpose 0.729 -> 0.675 ms, its
-# time-axis statistics 0.298 -> 0.301-0.305 ms, the step -2.8%
-# (profiles/r05s_pitch_prof.txt, r05s_pitch_ab.log; pitch sweep
-# r05t_pitch_sweep.txt).  Statistics over the last axis read the padded rows
-# in place (bm_reduce_rows), swaps / transposes and permuted reductions read
-# them with the pitch as the source row stride; any other use compacts the
-# rows once (_compact).  BOLT_AMD_ROW_PITCH=0 turns padding off; the
-# ALIGN / SKEW / PAD_DIV variables are the sweep's knobs (tools/pitch_sweep.sh).
+# start mid-line (C2's 2000 float32 = 8000 B: every other row), so
+# neighbouring tiles write parts of the same lines.  Such a result is stored
+# with its rows padded to a 256-B multiple (C2: 8192 B): the C2 transpose
+# 0.729 -> 0.675 ms, its time-axis statistics 0.298 -> 0.301-0.305 ms, the
+# step -2.8% (profiles/r05s_pitch_prof.txt, r05s_pitch_ab.log; pitch sweep
+# r05t_pitch_sweep.txt); other shapes gain more: float32 rows of 4400 B
+# 2.26 -> 1.65 ms, of 12000 B 1.34 -> 1.18, C4's uint16 .T (20000-B rows)
+# 9.2 -> 8.1 ms (r05zw_pitch_align.log: 256-B steps are the best or near it
+# everywhere; 1 KiB steps lose 8% on the uint16 rows).  Statistics over the
+# last axis read the padded rows in place (bm_reduce_rows); swaps,
+# transposes, indexing, map / filter / chunk of single-row records, column
+# statistics and elementwise ops read them too; the rest compacts the rows
+# once (_compact).  BOLT_AMD_ROW_PITCH=0 turns padding off; the ALIGN / SKEW /
+# PAD_DIV / MAX_GB variables are the sweeps' knobs (tools/pitch_sweep.sh,
+# tools/pitch_align_sweep.sh).
 ROW_PITCH = os.environ.get("BOLT_AMD_ROW_PITCH", "1") != "0"
 _PITCH_MIN_ROW = 4096            # bytes: shorter rows are not padded
-_PITCH_ALIGN = int(os.environ.get("BOLT_AMD_PITCH_ALIGN", 1024))  # bytes: padded rows start on this boundary
+_PITCH_ALIGN = int(os.environ.get("BOLT_AMD_PITCH_ALIGN", 256))  # bytes: padded rows start on this boundary
 _PITCH_SKEW = int(os.environ.get("BOLT_AMD_PITCH_SKEW", 0))       # bytes added to the aligned pitch (A/B knob)
 _PITCH_LINE = 128                # bytes: rows of a multiple of this stay dense
-_PITCH_PAD_DIV = int(os.environ.get("BOLT_AMD_PITCH_PAD_DIV", 32))  # at most 1/32 of a row is padding
-_PITCH_MAX_BYTES = 16 << 30      # larger results stay dense (compaction needs a second copy)
+_PITCH_PAD_DIV = int(os.environ.get("BOLT_AMD_PITCH_PAD_DIV", 16))  # at most 1/16 of a row is padding
+_PITCH_MAX_BYTES = int(os.environ.get("BOLT_AMD_PITCH_MAX_GB", 32)) << 30  # larger results stay dense (compaction needs a second copy)
 _PITCH_PLANS = {}  # (_move_plan, itemsize) -> None | pitched copy plan
 
 

@@ -51,10 +51,14 @@ def test_pitch_plan_thresholds():
     assert A._pitch_plan(_mv((2000, 512, 512), (1, 2, 0)), (2000, 512, 512), 8) is None
     # the last axis stays put: a row copy, rows written whole
     assert A._pitch_plan(_mv((4096, 256, 250), (1, 0, 2)), (4096, 256, 250), 4) is None
-    # short rows, and rows whose padding would exceed 1/32
+    # short rows and whole-line rows stay dense (with 256-B steps and rows of
+    # at least 4 KiB the padding stays under the 1/16 cap)
     assert A._pitch_plan(_mv((1000, 64), (1, 0)), (1000, 64), 2) is None
-    assert A._pitch_plan(_mv((1100, 64), (1, 0)), (1100, 64), 4) is None   # 4400 -> 5120 B
-    assert A._pitch_plan(_mv((8100, 64), (1, 0)), (8100, 64), 4) is not None  # 32400 -> 33792 B
+    assert A._pitch_plan(_mv((1024, 64), (1, 0)), (1024, 64), 4) is None      # 4096 B
+    assert A._pitch_plan(_mv((1100, 64), (1, 0)), (1100, 64), 4)[0] == 1152   # 4400 -> 4608 B
+    assert A._pitch_plan(_mv((1025, 64), (1, 0)), (1025, 64), 4)[0] == 1088   # 4100 -> 4352 B
+    assert A._pitch_plan(_mv((8100, 64), (1, 0)), (8100, 64), 4)[0] == 8128   # 32400 -> 32512 B
+    assert A._pitch_plan(_mv((10000, 64), (1, 0)), (10000, 64), 2)[0] == 10112  # C4's u16 rows: 20224 B
     # one row: nothing to align
     assert A._pitch_plan(_mv((2000, 1), (1, 0)), (2000, 1), 4) is None
 
