@@ -119,7 +119,9 @@ def _move_plan(shape, perm, split):
 # r05t_pitch_sweep.txt); other shapes gain more: float32 rows of 4400 B
 # 2.26 -> 1.65 ms, of 12000 B 1.34 -> 1.18, C4's uint16 .T (20000-B rows)
 # 9.2 -> 8.1 ms (r05zw_pitch_align.log: 256-B steps are the best or near it
-# everywhere; 1 KiB steps lose 8% on the uint16 rows).  Statistics over the
+# everywhere; 1 KiB steps lose 8% on the uint16 rows); rows of 2000 / 3000 B
+# +10-16%, but 1000-B rows padded to 1024 lose 16%, hence the 1536-B floor
+# (r05zz_short_rows.log).  Statistics over the
 # last axis read the padded rows in place (bm_reduce_rows); swaps,
 # transposes, indexing, map / filter / chunk of single-row records, column
 # statistics and elementwise ops read them too; the rest compacts the rows
@@ -127,7 +129,7 @@ def _move_plan(shape, perm, split):
 # PAD_DIV / MAX_GB variables are the sweeps' knobs (tools/pitch_sweep.sh,
 # tools/pitch_align_sweep.sh).
 ROW_PITCH = os.environ.get("BOLT_AMD_ROW_PITCH", "1") != "0"
-_PITCH_MIN_ROW = 4096            # bytes: shorter rows are not padded
+_PITCH_MIN_ROW = int(os.environ.get("BOLT_AMD_PITCH_MIN_ROW", 1536))  # bytes: shorter rows are not padded
 _PITCH_ALIGN = int(os.environ.get("BOLT_AMD_PITCH_ALIGN", 256))  # bytes: padded rows start on this boundary
 _PITCH_SKEW = int(os.environ.get("BOLT_AMD_PITCH_SKEW", 0))       # bytes added to the aligned pitch (A/B knob)
 _PITCH_LINE = 128                # bytes: rows of a multiple of this stay dense

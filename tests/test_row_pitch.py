@@ -51,9 +51,10 @@ def test_pitch_plan_thresholds():
     assert A._pitch_plan(_mv((2000, 512, 512), (1, 2, 0)), (2000, 512, 512), 8) is None
     # the last axis stays put: a row copy, rows written whole
     assert A._pitch_plan(_mv((4096, 256, 250), (1, 0, 2)), (4096, 256, 250), 4) is None
-    # short rows and whole-line rows stay dense (with 256-B steps and rows of
-    # at least 4 KiB the padding stays under the 1/16 cap)
-    assert A._pitch_plan(_mv((1000, 64), (1, 0)), (1000, 64), 2) is None
+    # short rows, rows whose padding would exceed 1/16 and whole-line rows stay dense
+    assert A._pitch_plan(_mv((250, 64), (1, 0)), (250, 64), 4) is None        # 1000 B
+    assert A._pitch_plan(_mv((1000, 64), (1, 0)), (1000, 64), 2)[0] == 1024   # 2000 -> 2048 B
+    assert A._pitch_plan(_mv((400, 64), (1, 0)), (400, 64), 4) is None        # 1600 -> 1792 B: > 1/16
     assert A._pitch_plan(_mv((1024, 64), (1, 0)), (1024, 64), 4) is None      # 4096 B
     assert A._pitch_plan(_mv((1100, 64), (1, 0)), (1100, 64), 4)[0] == 1152   # 4400 -> 4608 B
     assert A._pitch_plan(_mv((1025, 64), (1, 0)), (1025, 64), 4)[0] == 1088   # 4100 -> 4352 B

@@ -22,7 +22,11 @@ ctx = MI355XContext(device=dev)
 CASES = [("C2 f32 (2000,512,512) swap((0,),(0,1))", (2000, 512, 512), np.float32, lambda b: b.swap((0,), (0, 1))),
          ("f32 (3000,512,512) swap((0,),(0,1))", (3000, 512, 512), np.float32, lambda b: b.swap((0,), (0, 1))),
          ("C4 u16 (10000,1024,1024) .T", (10000, 1024, 1024), np.uint16, lambda b: b.T),
-         ("f32 (1100,2048,2048)/4 swap((0,),(0,1))", (1100, 1024, 1024), np.float32, lambda b: b.swap((0,), (0, 1)))]
+         ("f32 (1100,2048,2048)/4 swap((0,),(0,1))", (1100, 1024, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
+         ("f32 (250,4096,1024) swap: 1000-B rows", (250, 4096, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
+         ("f32 (500,2048,1024) swap: 2000-B rows", (500, 2048, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
+         ("f32 (750,2048,1024) swap: 3000-B rows", (750, 2048, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
+         ("u16 (1000,2048,2048) .T: 2000-B rows", (1000, 2048, 2048), np.uint16, lambda b: b.T)]
 
 
 def timed(f):
