@@ -26,7 +26,10 @@ CASES = [("C2 f32 (2000,512,512) swap((0,),(0,1))", (2000, 512, 512), np.float32
          ("f32 (250,4096,1024) swap: 1000-B rows", (250, 4096, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
          ("f32 (500,2048,1024) swap: 2000-B rows", (500, 2048, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
          ("f32 (750,2048,1024) swap: 3000-B rows", (750, 2048, 1024), np.float32, lambda b: b.swap((0,), (0, 1))),
-         ("u16 (1000,2048,2048) .T: 2000-B rows", (1000, 2048, 2048), np.uint16, lambda b: b.T)]
+         ("u16 (1000,2048,2048) .T: 2000-B rows", (1000, 2048, 2048), np.uint16, lambda b: b.T),
+         ("f64 (1500,1024,1024) swap: 12000-B rows", (1500, 1024, 1024), np.float64, lambda b: b.swap((0,), (0, 1))),
+         ("u8 (2000,1024,2048) .T: 2000-B rows", (2000, 1024, 2048), np.uint8, lambda b: b.T),
+         ("f64 (300,1024,1024) swap: 2400-B rows", (300, 1024, 1024), np.float64, lambda b: b.swap((0,), (0, 1)))]
 
 
 def timed(f):
