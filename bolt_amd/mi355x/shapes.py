@@ -41,8 +41,7 @@ class Keys(Shapes):
             return self._barray
         b = self._barray
         newshape = tuple(int(x) for x in new) + b.values.shape
-        data = _reslab(b, newshape)
-        return b._like(data, newshape, len(new))
+        return _relabel(b, newshape, len(new))
 
     def transpose(self, *axes):
         """Permute the key axes (shapes.py:66-89)."""
@@ -80,8 +79,7 @@ class Values(Shapes):
             return self._barray
         b = self._barray
         newshape = b.keys.shape + tuple(int(x) for x in new)
-        data = _reslab(b, newshape)
-        return b._like(data, newshape, b.split)
+        return _relabel(b, newshape, b.split)
 
     def transpose(self, *axes):
         """Permute the value axes (shapes.py:136-159)."""
@@ -99,6 +97,15 @@ class Values(Shapes):
 
     def __repr__(self):
         return str(self)
+
+
+def _relabel(b, newshape, split):
+    """``b``'s records under ``newshape`` (same C order).  A row-padded array
+    (one GPU) whose last axis keeps its length keeps its padded rows."""
+    d = b.__dict__
+    if "_pbuf" in d and len(newshape) >= 2 and newshape[-1] == b.shape[-1]:
+        return b._derive_padded(d["_pbuf"], d["_pitch"], newshape, split)
+    return b._like(_reslab(b, newshape), newshape, split)
 
 
 def _reslab(b, newshape):

@@ -217,6 +217,21 @@ def test_elementwise_reads_padded_rows(bctx, small_pitch):
     assert _padded(s)
 
 
+def test_reshapes_keep_padded_rows(bctx, small_pitch):
+    """Key reshapes (and value reshapes that keep the last axis) relabel the
+    padded rows; a value reshape of the last axis compacts."""
+    x = _data((41, 4, 6), np.float32, 8)
+    s = bolt.array(x, bctx).swap((0,), (0, 1))        # (4, 6, 41), split 2
+    want = np.ascontiguousarray(x.transpose(1, 2, 0))
+    k = s.keys.reshape((24,))
+    assert _padded(k) and k.shape == (24, 41) and k.toarray().tobytes() == want.tobytes()
+    t = bolt.array(x, bctx).transpose(1, 2, 0)        # (4, 6, 41), split 1
+    v = t.values.reshape((2, 3, 41))
+    assert _padded(v) and v.shape == (4, 2, 3, 41) and v.toarray().tobytes() == want.tobytes()
+    w = t.values.reshape((246,))
+    assert not _padded(w) and w.toarray().tobytes() == want.tobytes()
+
+
 def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
     monkeypatch.setattr(A, "ROW_PITCH", False)
     x = _data((41, 3, 5), np.float32)
