@@ -932,6 +932,10 @@ class BoltArrayMI355X(BoltArray):
             return self
         shape = tuple(d for i, d in enumerate(self._shape) if i not in drop)
         split = len([d for d in range(self._split) if d not in drop])
+        d = self.__dict__
+        if "_pbuf" in d and len(shape) >= 2 and (self.ndim - 1) not in drop:
+            # unit axes only: a padded array's rows stay as they are
+            return self._derive_padded(d["_pbuf"], d["_pitch"], shape, split)
         data = self._data
         if 0 in drop and self._ctx.world_size > 1:
             # the leading axis goes: re-slab on the new one (a 0-d result lives on rank 0)

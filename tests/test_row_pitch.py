@@ -218,8 +218,8 @@ def test_elementwise_reads_padded_rows(bctx, small_pitch):
 
 
 def test_reshapes_keep_padded_rows(bctx, small_pitch):
-    """Key reshapes (and value reshapes that keep the last axis) relabel the
-    padded rows; a value reshape of the last axis compacts."""
+    """Key reshapes, value reshapes that keep the last axis and squeezes
+    relabel the padded rows; a value reshape of the last axis compacts."""
     x = _data((41, 4, 6), np.float32, 8)
     s = bolt.array(x, bctx).swap((0,), (0, 1))        # (4, 6, 41), split 2
     want = np.ascontiguousarray(x.transpose(1, 2, 0))
@@ -230,6 +230,10 @@ def test_reshapes_keep_padded_rows(bctx, small_pitch):
     assert _padded(v) and v.shape == (4, 2, 3, 41) and v.toarray().tobytes() == want.tobytes()
     w = t.values.reshape((246,))
     assert not _padded(w) and w.toarray().tobytes() == want.tobytes()
+    u = bolt.array(x.reshape(41, 1, 4, 6), bctx, axis=(0, 1)).transpose(1, 2, 3, 0)  # (1, 4, 6, 41), split 2
+    assert _padded(u)
+    q = u.squeeze(0)
+    assert _padded(q) and q.shape == (4, 6, 41) and q.toarray().tobytes() == want.tobytes()
 
 
 def test_row_pitch_off_is_dense(bctx, small_pitch, monkeypatch):
