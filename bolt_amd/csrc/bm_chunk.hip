@@ -397,9 +397,9 @@ __global__ void __launch_bounds__(kCThreads)
         // wrong bytes, never an access outside run b of a source record of
         // this group: k in [0, group), the offset in [0, len)
         k = k < 0 ? 0 : (k >= group ? group - 1 : k);
-        int64_t w = off - k * len;
-        w = w < 0 ? 0 : (w >= len ? len - 1 : w);
-        const V *sp = s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + w;
+        int64_t pos = off - k * len;
+        pos = pos < 0 ? 0 : (pos >= len ? len - 1 : pos);
+        const V *sp = s + ((int64_t)g * group + k) * src_rec + tab[4 * lo] + pos;
         x[u] = *sp;  // temporal: the shared line's second read hits L2
       }
     }

@@ -35,32 +35,26 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: grid * block threads < 2^32
-#ifndef BM_COLS_UNROLL
-#define BM_COLS_UNROLL 8  // rows in flight per lane in the column reductions: 8 over 4 +1.2-1.4% on the 64 GiB target mean / std and C2-shape columns, 2 -4-8% (profiles/r02_ab_cols.log)
-#endif
-#ifndef BM_COLS_BLOCKS
-#define BM_COLS_BLOCKS 2048  // split R over blocks below this many column tiles (A/B knob)
-#endif
-#ifndef BM_COLS_TCV
-#define BM_COLS_TCV 256  // column vectors per block at most; the rest of the 256 lanes are row phases (A/B knob)
-#endif
-#ifndef BM_COLS_TCV_MIN
-#define BM_COLS_TCV_MIN 64  // narrowest tile taken to reach BM_COLS_BLOCKS before chunking R (A/B knob)
-#endif
-constexpr int kColsUnroll = BM_COLS_UNROLL;
-#ifndef BM_ROWS_UNROLL
-#define BM_ROWS_UNROLL 2  // A/B on C2 rows: 2 beats 4 by 4%, 8 by 25% (profiles/r01_ab1.log)
-#endif
-constexpr int kRowsUnroll = BM_ROWS_UNROLL;  // 16-B vectors in flight per lane (rows kernel)
-#ifndef BM_INT_UNROLL
-#define BM_INT_UNROLL 8  // exact-integer column var: rows in flight per lane (C4 var 3.76 -> 3.47 ms over 4, profiles/r02_ab_int.log)
-#endif
-#ifndef BM_RED_XCD
-#define BM_RED_XCD 1  // rows kernel: blocks dealt to one XCD take consecutive rows (C2 mean / std +3-4%, profiles/r02_ab_redxcd.log)
-#endif
-#ifndef BM_COLS_XCD
-#define BM_COLS_XCD 1  // column kernels: blocks dealt to one XCD take consecutive column tiles (C4 var +1.1%, 64 GiB-target-shaped mean / std over axis 0 +2.2% / +1.6%, profiles/r05h_ab_cols_xcd.log)
-#endif
+// Shipped parameters (the A/B runs that chose them are cited; the rejected
+// values live in git history and tools/microbench/):
+// rows in flight per lane in the column reductions: 8 over 4 +1.2-1.4% on the
+// 64 GiB target mean / std and C2-shape columns, 2 -4-8% (profiles/r02_ab_cols.log)
+constexpr int kColsUnroll = 8;
+// split R over blocks below this many column tiles; column vectors per block
+// at most (the rest of the 256 lanes are row phases); the narrowest tile taken
+// to reach kColsBlocks before chunking R (profiles/r03zb_ab_tcv.log, r03zc_ab_tcv_rule.log)
+constexpr int64_t kColsBlocks = 2048;
+constexpr int64_t kColsTcv = 256;
+constexpr int64_t kColsTcvMin = 64;
+// 16-B vectors in flight per lane in the rows kernel: 2 beats 4 by 4%, 8 by 25%
+// (profiles/r01_ab1.log; 3: equal, 4: -5% again on padded rows, r05z_rows_unroll.txt)
+constexpr int kRowsUnroll = 2;
+// exact-integer column var: rows in flight per lane (C4 var 3.76 -> 3.47 ms over 4, profiles/r02_ab_int.log)
+constexpr int kIntUnroll = 8;
+// rows kernel: blocks dealt to one XCD take consecutive rows (C2 mean / std
+// +3-4%, profiles/r02_ab_redxcd.log); column kernels: blocks dealt to one XCD
+// take consecutive column tiles (C4 var +1.1%, 64 GiB-target-shaped mean / std
+// over axis 0 +2.2% / +1.6%, profiles/r05h_ab_cols_xcd.log)
 
 enum Mode {
   M_MEAN = 0, M_MOM = 1, M_FSUM = 2, M_ISUM = 3, M_OR = 4, M_MAX = 5, M_MIN = 6,
@@ -421,17 +415,15 @@ __device__ __forceinline__ void emit(const Sink &sk, int64_t e, double n, double
 
 // ------------------------------------------------------------------ cols --
 // blockIdx.x, with the blocks the hardware deals to one XCD (every 8th)
-// remapped to consecutive indices when BM_COLS_XCD (a bijection of the grid):
+// remapped to consecutive indices (a bijection of the grid):
 // each XCD then reads one contiguous range of every row
 // (the rows kernel's rotated start, rows_block, does not help the columns:
 // -0.1...-0.6% on the 64 GiB target / C4 / C2 column statistics,
 // profiles/r05zf_ab_colskew.log)
 __device__ __forceinline__ uint64_t xcd_block() {
   uint64_t bid = blockIdx.x;
-  if (BM_COLS_XCD) {
-    const uint64_t g8 = gridDim.x / 8 * 8;
-    if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
-  }
+  const uint64_t g8 = gridDim.x / 8 * 8;
+  if (bid < g8) bid = (bid % 8) * (g8 / 8) + bid / 8;
   return bid;
 }
 
@@ -665,17 +657,13 @@ __global__ void __launch_bounds__(kThreads)
 // and wraps, so the eight XCDs are never a power-of-two distance apart: on
 // C2's padded rows (8192-B pitch, eighths 256 MiB apart) mean / std
 // -1.2% / -1.0% over 3 alternating rounds (profiles/r05zd_xcd_skew.txt)
-#ifndef BM_RED_XCD_SKEW
-#define BM_RED_XCD_SKEW 37
-#endif
+constexpr uint64_t kRedXcdSkew = 37;
 __device__ __forceinline__ uint64_t rows_block() {
   uint64_t bid = blockIdx.x;
-  if (BM_RED_XCD) {
-    const uint64_t g8 = gridDim.x / 8 * 8;
-    if (bid < g8) {
-      const uint64_t E = g8 / 8;
-      bid = (bid % 8) * E + (BM_RED_XCD_SKEW ? (bid / 8 + (bid % 8) * BM_RED_XCD_SKEW) % E : bid / 8);
-    }
+  const uint64_t g8 = gridDim.x / 8 * 8;
+  if (bid < g8) {
+    const uint64_t E = g8 / 8;
+    bid = (bid % 8) * E + (bid / 8 + (bid % 8) * kRedXcdSkew) % E;
   }
   return bid;
 }
@@ -715,37 +703,64 @@ __global__ void __launch_bounds__(kThreads)
   // var / std: every value is shifted by the row's first element P (shared
   // by all chunks of the row), so the Welford means stay near zero and keep
   // their digits on offset data (1e6 + N(0,1)); batches bound outliers.
-  if (MODE == M_MEAN) acc.pivot(to_f64(row[r_lo]));
-  const double P = (MODE == M_MOM) ? to_f64(row[0]) : 0.0;
-  // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
-  for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
-    T v[kRowsUnroll][VEC];
+  //
+  // The pivots are lane 0's first element.  Where lane 0 runs the main loop,
+  // its first load is peeled and the pivot broadcast from it: a separate
+  // element load of the row's first line would be a second HBM read of it
+  // (that load is temporal, the vector loads non-temporal).
+  double P = 0.0;
+  T v[kRowsUnroll][VEC];
+  const bool peel = (MODE == M_MEAN || MODE == M_MOM) &&
+                    r_lo + VEC + (int64_t)(kRowsUnroll - 1) * stride <= r_hi;
+  bool have = false;
+  if (peel) {
+    if (j + VEC + (kRowsUnroll - 1) * stride <= r_hi) {
 #pragma unroll
-    for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
+      for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
+      have = true;
+    }
+    const double first = __shfl(have ? to_f64(v[0][0]) : 0.0, 0, 64);
+    if (MODE == M_MEAN) acc.pivot(first);
+    if (MODE == M_MOM) P = (r_lo == 0) ? first : to_f64(row[0]);
+  } else {
+    if (MODE == M_MEAN) acc.pivot(to_f64(row[r_lo]));
+    if (MODE == M_MOM) P = to_f64(row[0]);
+  }
+  auto consume = [&](T (&vv)[kRowsUnroll][VEC]) {
     if constexpr (MODE == M_MOM) {
       // the kRowsUnroll * VEC values in hand form one Welford batch
       double x[kRowsUnroll * VEC];
 #pragma unroll
       for (int u = 0; u < kRowsUnroll; ++u)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) x[u * VEC + k] = to_f64(v[u][k]);
+        for (int k = 0; k < VEC; ++k) x[u * VEC + k] = to_f64(vv[u][k]);
       w.add_main<kRowsUnroll * VEC>(x, P);
-      continue;
+      return;
     }
 #pragma unroll
     for (int u = 0; u < kRowsUnroll; ++u) {
       if constexpr (MODE == M_MEAN && VEC % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < VEC; k += 2) acc.add2(to_f64(v[u][k]), to_f64(v[u][k + 1]));
+        for (int k = 0; k < VEC; k += 2) acc.add2(to_f64(vv[u][k]), to_f64(vv[u][k + 1]));
         continue;
       }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (MODE == M_MEAN) acc.add(to_f64(v[u][k]));
-        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(v[u][k]));
-        else us = bop<T, MODE>(us, belem<T, MODE>(v[u][k]));
+        if (MODE == M_MEAN) acc.add(to_f64(vv[u][k]));
+        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(vv[u][k]));
+        else us = bop<T, MODE>(us, belem<T, MODE>(vv[u][k]));
       }
     }
+  };
+  if (have) {
+    consume(v);
+    j += kRowsUnroll * stride;
+  }
+  // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
+  for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
+#pragma unroll
+    for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
+    consume(v);
   }
   // var / std: the rest of the row and the cross-lane merge run as sums
   // around one wave-wide pivot C = lane 0's Welford mean (lane 0 holds 1/64
@@ -898,7 +913,7 @@ __global__ void __launch_bounds__(kThreads)
   if (active) {
     const T *base = src + ((int64_t)o * d.R) * d.I + col0;
     int64_t r = r_lo + ph;
-    constexpr int U = BM_INT_UNROLL;  // rows in flight per lane
+    constexpr int U = kIntUnroll;  // rows in flight per lane
     for (; r + (U - 1) * nph < r_hi; r += U * nph) {
       T v[U][VEC];
 #pragma unroll
@@ -1242,19 +1257,19 @@ RedPlan plan_reduce(int dt, int64_t O, int64_t R, int64_t I, const void *src, in
     p.vec = vec;
     const int64_t ncolv = cdiv(I, vec);
     int tcv = 1;
-    while (tcv < BM_COLS_TCV && tcv < ncolv) tcv <<= 1;
+    while (tcv < kColsTcv && tcv < ncolv) tcv <<= 1;
     // narrower column tiles (more row phases merged in LDS) before splitting
     // R into chunks that need a workspace and a combine launch: C4's uint16
     // var over axis 0 3.50 -> 3.17 ms with 64-vector tiles and no chunks
     // (profiles/r03zb_ab_tcv.log); the float C2 column statistics move +-2%
-    while (tcv > BM_COLS_TCV_MIN && O * cdiv(ncolv, tcv) < BM_COLS_BLOCKS) tcv >>= 1;
+    while (tcv > kColsTcvMin && O * cdiv(ncolv, tcv) < kColsBlocks) tcv >>= 1;
     p.tcv = tcv;
     p.nph = 256 / tcv;
     p.ntc = cdiv(ncolv, tcv);
     const int64_t blocks = O * p.ntc;
     int64_t nch = 1;
-    if (blocks < BM_COLS_BLOCKS) {
-      nch = cdiv(BM_COLS_BLOCKS, blocks);
+    if (blocks < kColsBlocks) {
+      nch = cdiv(kColsBlocks, blocks);
       const int64_t maxch = std::max<int64_t>(1, R / ((int64_t)p.nph * 8));
       nch = std::min(nch, maxch);
     }
@@ -1413,10 +1428,8 @@ int launch_main(int mode, int dt, const RedPlan &p, const void *src, int64_t O, 
   }
 }
 
-#ifndef BM_COMB_BLK
-#define BM_COMB_BLK 1  // block-per-output combine for few outputs and many parts (0 = off; A/B knob)
-#endif
-bool comb_blk(const CombDesc &cd) { return BM_COMB_BLK && cd.nout <= 1024 && cd.nparts >= 8; }
+// block-per-output combine for few outputs from many parts
+bool comb_blk(const CombDesc &cd) { return cd.nout <= 1024 && cd.nparts >= 8; }
 
 template <int MODE, typename T>
 void launch_combine_k(int g, const double *p0, const double *p1, const CombDesc &cd, Sink sk, hipStream_t st) {

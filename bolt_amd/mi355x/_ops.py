@@ -54,9 +54,8 @@ def record_parts(rmap, src_rec, es, part_bytes=None):
     ``part_bytes`` of LDS, as a flat [dlo, dhi, slo, shi, ...] list ([] = one
     whole-record tile).  Ranges are 16-B aligned; the split is taken only if
     the staged bytes stay within 1.25x of the record (halo rows re-read)."""
-    import os
     part_bytes = PART_BYTES if part_bytes is None else part_bytes
-    if os.environ.get("BOLT_AMD_RECMAP_PARTS", "1") == "0" or src_rec * es <= part_bytes:
+    if src_rec * es <= part_bytes:
         return []
     al = max(1, 16 // es)
     n = rmap.size
@@ -85,8 +84,7 @@ def stage_mask(rmap, parts, es):
     source range [slo, shi) that its map entries read, or (None, 0) when there
     are no parts or the mask would skip less than STAGE_MASK_MIN_SKIP of the
     staged units (values_to_keys skips the moved axis' halo rows: ~16% on C5)."""
-    import os
-    if not parts or os.environ.get("BOLT_AMD_STAGE_MASK", "1") == "0":  # A/B knob
+    if not parts:
         return None, 0
     p4 = np.asarray(parts, dtype=np.int64).reshape(-1, 4)
     units = [(-(-(int(shi - slo) * es) // 16)) for _, _, slo, shi in p4]

@@ -28,7 +28,7 @@ from bolt_amd.mi355x.context import local_shape
 from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, gather_to_host, permute_sharded, redistribute_rows, select_sharded, _empty
 from bolt_amd.mi355x.transfer import finish_host_result, host_result, to_device, to_host
 from bolt_amd.local import BoltArrayLocal
-from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, reduce_layout, stat_dtype
+from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, swap_shape, reduce_layout, stat_dtype
 from bolt_amd.utils import tupleize, argpack, inshape, istransposeable, isreshapeable
 
 _STAT_CODES = {'mean': _lib.STAT_MEAN, 'variance': _lib.STAT_VAR, 'stdev': _lib.STAT_STD}
@@ -96,7 +96,7 @@ def _check_swap_plan(vshape, dtype, size):
         raise type(err)(*err.args)
 
 
-_SWAP_PLANS = {}   # (shape, split, dtype, kaxes, vaxes, size) -> _move_plan | _NOOP
+_SWAP_PLANS = {}   # (shape, split, dtype, kaxes, vaxes, size) -> (_move_plan, squeezed shape | None) | _NOOP
 _NOOP = object()
 
 
@@ -125,16 +125,14 @@ def _move_plan(shape, perm, split):
 # last axis read the padded rows in place (bm_reduce_rows); swaps,
 # transposes, indexing, map / filter / chunk of single-row records, column
 # statistics and elementwise ops read them too; the rest compacts the rows
-# once (_compact).  BOLT_AMD_ROW_PITCH=0 turns padding off; the ALIGN / SKEW /
-# PAD_DIV / MAX_GB variables are the sweeps' knobs (tools/pitch_sweep.sh,
-# tools/pitch_align_sweep.sh).
-ROW_PITCH = os.environ.get("BOLT_AMD_ROW_PITCH", "1") != "0"
-_PITCH_MIN_ROW = int(os.environ.get("BOLT_AMD_PITCH_MIN_ROW", 1536))  # bytes: shorter rows are not padded
-_PITCH_ALIGN = int(os.environ.get("BOLT_AMD_PITCH_ALIGN", 256))  # bytes: padded rows start on this boundary
-_PITCH_SKEW = int(os.environ.get("BOLT_AMD_PITCH_SKEW", 0))       # bytes added to the aligned pitch (A/B knob)
-_PITCH_LINE = 128                # bytes: rows of a multiple of this stay dense
-_PITCH_PAD_DIV = int(os.environ.get("BOLT_AMD_PITCH_PAD_DIV", 16))  # at most 1/16 of a row is padding
-_PITCH_MAX_BYTES = int(os.environ.get("BOLT_AMD_PITCH_MAX_GB", 32)) << 30  # larger results stay dense (compaction needs a second copy)
+# once (_compact).  ROW_PITCH = False turns padding off (the tests' switch;
+# the sweeps that chose the constants ran on round-5 builds with them as
+# environment knobs: tools/pitch_sweep.sh, tools/pitch_align_sweep.sh).
+ROW_PITCH = True
+_PITCH_MIN_ROW = 1536   # bytes: shorter rows are not padded
+_PITCH_ALIGN = 256      # bytes: padded rows start on this boundary
+_PITCH_LINE = 128       # bytes: rows of a multiple of this stay dense
+_PITCH_PAD_DIV = 16     # at most 1/16 of a row is padding
 _PITCH_PLANS = {}  # (_move_plan, itemsize) -> None | pitched copy plan
 
 
@@ -150,17 +148,41 @@ def _pitch_plan(mv, shape, es):
     rb = R * es
     if rb < _PITCH_MIN_ROW or rb % _PITCH_LINE == 0:
         return None
-    pb = -(-rb // _PITCH_ALIGN) * _PITCH_ALIGN + _PITCH_SKEW
+    pb = -(-rb // _PITCH_ALIGN) * _PITCH_ALIGN
     if (pb - rb) * _PITCH_PAD_DIV > rb or pb % es:
         return None
     P = pb // es
     rows = int(np.prod(new_shape[:-1], dtype=np.int64))
-    if rows * pb > _PITCH_MAX_BYTES or rows < 2:
+    if rows < 2:
         return None
     sstr = [1] * len(shape)
     for k in range(len(shape) - 2, -1, -1):
         sstr[k] = sstr[k + 1] * shape[k + 1]
     return P, rows, list(new_shape), [sstr[p] for p in perm], _padded_strides(new_shape, P)
+
+
+_DEVICE_BYTES = {}  # device index -> total HBM bytes
+
+
+def _pitch_fits(pp, es, device):
+    """Room for the padded result AND a later dense compaction of it (a
+    consumer that needs dense records copies them once, see _compact): checked
+    against the device's free memory (plus what torch's allocator holds
+    unused) only when the two together exceed 1/8 of the device, so the small
+    results of a hot loop never query the driver."""
+    if device.type != "cuda":
+        return True
+    import torch
+    P, rows, oshape = pp[0], pp[1], pp[2]
+    need = rows * (P + oshape[-1]) * es
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    total = _DEVICE_BYTES.get(idx)
+    if total is None:
+        total = _DEVICE_BYTES[idx] = torch.cuda.get_device_properties(idx).total_memory
+    if need * 8 <= total:
+        return True
+    free = torch.cuda.mem_get_info(idx)[0] + torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
+    return need <= free
 
 
 def _padded_strides(shape, P):
@@ -175,7 +197,7 @@ def _padded_strides(shape, P):
 
 
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
-_STAT_AXES = {}  # (shape, axis as given) -> (validated axis tuple, records after _align)
+_STAT_AXES = {}  # (shape, split, axis as given) -> (validated axes, records after _align, record shape | None)
 
 
 class BoltArrayMI355X(BoltArray):
@@ -416,6 +438,8 @@ class BoltArrayMI355X(BoltArray):
                     _PITCH_PLANS.clear()
                 _PITCH_PLANS[key] = pp
             d = self.__dict__
+            if pp is not None and not _pitch_fits(pp, es, self._device):
+                pp = None
             if "_pbuf" in d:
                 # a padded source is read in place: its strides, permuted
                 src, pstr = d["_pbuf"], _padded_strides(self._shape, d["_pitch"])
@@ -474,7 +498,13 @@ class BoltArrayMI355X(BoltArray):
             hit = _SWAP_PLANS.get(key) if key is not None else None
             if hit is None:
                 plan = self._swap_plan(kaxes, vaxes, size)
-                hit = _NOOP if plan is None else _move_plan(self._shape, *plan)
+                if plan is None:
+                    hit = _NOOP
+                else:
+                    mv = _move_plan(self._shape, *plan[:2])
+                    ref = swap_shape(self._shape, self._split, *plan[2:])
+                    # the reference's unit-axis squeezes (plan.swap_shape): a relabel
+                    hit = (mv, ref[0] if ref is not None and ref[0] != mv[2] else None)
             if len(_SWAP_PLANS) > 4096:
                 _SWAP_PLANS.clear()
             for k in (key, raw):
@@ -482,7 +512,17 @@ class BoltArrayMI355X(BoltArray):
                     _SWAP_PLANS[k] = hit
         if hit is _NOOP:
             return self
-        return self._move(hit)
+        mv, squeezed = hit
+        out = self._move(mv)
+        return out if squeezed is None else out._relabel(squeezed)
+
+    def _relabel(self, shape):
+        """The same records under ``shape`` -- this shape with unit axes
+        dropped, split unchanged (the reference's swap squeezes)."""
+        d = self.__dict__
+        if "_pbuf" in d and len(shape) >= 2 and shape[-1] == self._shape[-1]:
+            return self._derive_padded(d["_pbuf"], d["_pitch"], shape, self._split)
+        return self._derive(self._data, shape, self._split)
 
     def _swap_plan(self, kaxes, vaxes, size):
         """Validation and net permutation of swap: (perm, newsplit), or None for a no-op."""
@@ -513,7 +553,7 @@ class BoltArrayMI355X(BoltArray):
         kaxes = [int(k) % self._split for k in kaxes]
         vaxes = [int(v) % nv for v in vaxes] if nv else []
 
-        return swap_perm(self.ndim, self._split, kaxes, vaxes)
+        return swap_perm(self.ndim, self._split, kaxes, vaxes) + (kaxes, vaxes)
 
     def transpose(self, *axes):
         """Permute the axes, split unchanged (array.py:765-808)."""
@@ -1067,26 +1107,28 @@ class BoltArrayMI355X(BoltArray):
     def _stat(self, axis=None, func=None, name=None, keepdims=False):
         """Statistic over ``axis`` (array.py:284-334); results are host arrays / scalars."""
         if name and not func:
-            try:  # axes already validated for this shape, keyed by the argument as given
-                ak = (self._shape, axis)
+            try:  # axes already validated for this shape and split, keyed by the argument as given
+                ak = (self._shape, self._split, axis)
                 hit = _STAT_AXES.get(ak)
             except TypeError:  # unhashable axis (a list)
                 ak = hit = None
             if hit is None:
                 ax = tupleize(list(range(len(self.shape))) if axis is None else axis)
                 inshape(self.shape, ax)
-                hit = (ax, self._nrecords(ax))
+                hit = (ax, self._nrecords(ax), self._aligned_vshape(ax))
                 if ak is not None:
                     if len(_STAT_AXES) > 4096:
                         _STAT_AXES.clear()
                     _STAT_AXES[ak] = hit
-            axis, nrec = hit
+            axis, nrec, vs = hit
             if nrec == 0:
                 # no records after _align: the merged StatCounter is the empty one
                 # (statcounter.py:28-41, :109-130): mean 0.0, variance / stdev nan
                 arr = 0.0 if name == 'mean' else float('nan')
             else:
                 arr, _ = self._reduced(axis, _STAT_CODES[name])
+                if vs is not None:
+                    arr = arr.reshape(vs)
                 if arr.ndim == 0:
                     arr = arr[()]
             if keepdims:
@@ -1120,15 +1162,18 @@ class BoltArrayMI355X(BoltArray):
         if nrec == 0:
             raise ValueError("Can not reduce() empty RDD")  # treeReduce of no records (array.py:269)
         stat = _UFUNC_STATS.get(func) if _hashable(func) else None
+        vs = self._aligned_vshape(axis)
         if nrec == 1:
             # treeReduce of one record returns it untouched (no func call)
             kept = [d for i, d in enumerate(self._shape) if i not in set(int(a) for a in axis)]
-            arr = self.toarray().reshape(kept)
+            arr = self.toarray().reshape(kept if vs is None else vs)
         elif stat is not None and self._reduce_dtype_ok(func, stat):
             arr, _ = self._reduced(axis, stat)
         else:
             from bolt_amd.mi355x.functional import user_fn
-            arr = self._tree_reduce(user_fn(func), axis)
+            arr = self._tree_reduce(user_fn(func), axis, vs)
+        if vs is not None:
+            arr = arr.reshape(vs)
         if arr.ndim == 0:
             arr = arr[()]
         if keepdims:
@@ -1147,8 +1192,10 @@ class BoltArrayMI355X(BoltArray):
         want = np.dtype(bool) if stat in (_lib.STAT_LAND, _lib.STAT_LOR) else self._dtype
         return probe.dtype == want
 
-    def _tree_reduce(self, func, axis):
-        """Pairwise tree of a user function over the aligned records, on the device."""
+    def _tree_reduce(self, func, axis, vshape=None):
+        """Pairwise tree of a user function over the aligned records, on the
+        device; ``vshape``: the records' shape when the reference's _align
+        squeezes a unit axis (see _aligned_vshape)."""
         import torch
         from bolt_amd.mi355x.functional import view, apply_pairs, numpy_dtype
         ctx = self._ctx
@@ -1176,7 +1223,7 @@ class BoltArrayMI355X(BoltArray):
             if src.numel():
                 self._backend.permute(src, lshape, perm, self._dtype.itemsize, tmp)
             src = tmp
-        rec_shape = tuple(lshape[i] for i in kept)
+        rec_shape = tuple(lshape[i] for i in kept) if vshape is None else tuple(vshape)
         recs = view(src, (O, R, I), self._dtype).permute(1, 0, 2).reshape((R,) + rec_shape)
         if R:
             part = _tree(func, recs)
@@ -1196,6 +1243,21 @@ class BoltArrayMI355X(BoltArray):
         has = [r for r, (lo, hi) in enumerate(ctx.bounds(gshape[0])) if hi > lo]
         res = _tree(func, per[has])
         return res.cpu().numpy().astype(numpy_dtype(res.dtype), copy=False)
+
+    def _aligned_vshape(self, axis):
+        """The record shape after the reference's _align(axis) (array.py:85-115)
+        when its swap squeezes a unit axis (plan.swap_shape), else None: the
+        kept axes' extents in ascending order."""
+        tokeys = [a - self._split for a in axis if a >= self._split]
+        tovalues = [a for a in range(self._split) if a not in axis]
+        if not (tokeys or tovalues):
+            return None
+        ref = swap_shape(self._shape, self._split, tovalues, tokeys)
+        if ref is None:
+            return None
+        vs = ref[0][ref[1]:]
+        kept = tuple(d for i, d in enumerate(self._shape) if i not in set(int(a) for a in axis))
+        return None if vs == kept else vs
 
     def _nrecords(self, axis):
         """Records the reduction sees after _align: the product of the reduced extents."""
@@ -1235,12 +1297,40 @@ class BoltArrayMI355X(BoltArray):
         slabs are gathered window by window (dist.gather_to_host): device
         memory per rank stays at its slab plus one window."""
         ctx = self._ctx
+        if "_pbuf" in self.__dict__:
+            return self._padded_to_host()
         if ctx.world_size == 1:
             return to_host(self._data, self._dtype, self._shape)
         rowbytes = int(np.prod(self._shape[1:], dtype=np.int64)) * self._dtype.itemsize
         rows = self._shape[0] if self._shape else 1  # a 0-d array lives on rank 0
         sizes = [(hi - lo) * rowbytes for lo, hi in ctx.bounds(rows)]
         return gather_to_host(ctx, self._data, sizes).view(self._dtype).reshape(self._shape)
+
+    def _padded_to_host(self):
+        """toarray of a row-padded array (one GPU): the rows are compacted
+        window by window into two device windows of at most transfer.CHUNK
+        bytes, each DMA'd to page-locked memory while the next is compacted
+        -- no dense copy of the whole array on the device (array.py:1006-1014)."""
+        from bolt_amd.mi355x import transfer
+        d = self.__dict__
+        pbuf, P = d["_pbuf"], d["_pitch"]
+        es = self._dtype.itemsize
+        R = self._shape[-1]
+        rows = int(np.prod(self._local_shape[:-1], dtype=np.int64))
+        rb = R * es
+        out = np.empty(rows * rb, dtype=np.uint8)
+        if rows == 0 or rb == 0:
+            return out.view(self._dtype).reshape(self._shape)
+        wrows = max(1, min(rows, transfer.CHUNK // rb)) if pbuf.device.type == "cuda" else rows
+        be = backend_for(pbuf.device)
+        wins = [_empty(wrows * rb, pbuf.device) for _ in range(2 if rows > wrows else 1)]
+
+        def produce(lo, hi, k):
+            r0, r1 = lo // rb, hi // rb
+            be.copy_strided(pbuf, r0 * P * es, wins[k], 0, [r1 - r0, R], [P, 1], [R, 1], es)
+            return wins[k][:(r1 - r0) * rb]
+        transfer.copy_to_host(pbuf, out, produce=produce, chunk=wrows * rb)
+        return out.view(self._dtype).reshape(self._shape)
 
     def tolocal(self):
         """As a local bolt array (array.py:999-1004)."""

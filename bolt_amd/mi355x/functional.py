@@ -43,12 +43,22 @@ def user_fn(func):
     """``func`` as the mode hands it records: torch has no arithmetic for
     uint16 / uint32 (2.10: add, comparisons, max, neg raise NotImplementedError),
     where the reference's numpy records compute in the fixed-width type.  Such
-    tensors reach ``func`` widened to int32 / int64 (every value exact), and a
-    result in the widened type comes back in the record type: numpy's
-    wrap-around for + - * & | ^ <<, exact for comparisons, min / max and //.
+    tensors reach ``func`` widened to int64 (every value exact), and the
+    result's dtype is put back to numpy's:
+      * when ``func`` also runs on a numpy record of the same shape and dtype
+        (a zero record, once per shape; most record functions do), the result
+        takes the dtype numpy gives -- uint32 for ``v * 2`` (wrap-around),
+        uint64 for ``v.sum()``, int64 for an explicit ``astype(int64)``; a
+        torch-only function that runs on an unwidened zero record (an
+        explicit ``v.to(torch.int64)``) keeps torch's dtype for it;
+      * otherwise a result of the record's own shape in the widened type is
+        elementwise and comes back in the record type (numpy's wrap-around for
+        + - * & | ^ <<, exact for comparisons, min / max and //); any other
+        result keeps the widened type (exact).
     Keys (``with_keys`` pairs) pass through; other dtypes are untouched."""
     import torch
-    wide = {torch.uint16: torch.int32, torch.uint32: torch.int64}
+    wide = {torch.uint16: torch.int64, torch.uint32: torch.int64}
+    probes = {}
 
     def widen(a):
         if isinstance(a, torch.Tensor) and a.dtype in wide:
@@ -59,6 +69,36 @@ def user_fn(func):
             return type(a)(x for x, _ in parts) if type(a) is tuple else a, orig
         return a, None
 
+    def numpy_dtype_of(shape, orig):
+        """The result dtype of func on a zero record of the record's own dtype:
+        numpy's where func takes ndarrays, else torch's where func needs no
+        arithmetic torch lacks (an explicit cast, a view), else None."""
+        key = (tuple(shape), orig)
+        if key not in probes:
+            probes[key] = None
+            try:
+                with np.errstate(all="ignore"):
+                    r = func(np.zeros(tuple(shape), dtype=numpy_dtype(orig)))
+                if isinstance(r, (np.ndarray, np.generic)):
+                    probes[key] = np.asarray(r).dtype
+            except Exception:  # a torch-only function
+                pass
+            if probes[key] is None:
+                try:
+                    r = func(torch.zeros(tuple(shape), dtype=orig))
+                    if isinstance(r, torch.Tensor):
+                        probes[key] = numpy_dtype(r.dtype)
+                except Exception:  # needs the widened arithmetic
+                    pass
+        return probes[key]
+
+    def record_shape(a):
+        if isinstance(a, torch.Tensor):
+            return tuple(a.shape)
+        if isinstance(a, tuple) and not isinstance(a, KeyTuple):
+            return next((s for s in map(record_shape, a) if s is not None), None)
+        return None
+
     def wrapped(*args):
         new, orig = [], None
         for a in args:
@@ -66,9 +106,14 @@ def user_fn(func):
             new.append(w)
             orig = orig or o
         out = func(*new)
-        if orig is not None and isinstance(out, torch.Tensor) and out.dtype == wide[orig]:
-            return out.to(orig)
-        return out
+        if orig is None or not isinstance(out, torch.Tensor) or out.dtype != wide[orig]:
+            return out
+        if len(args) == 1 and isinstance(args[0], torch.Tensor):
+            want = numpy_dtype_of(args[0].shape, orig)
+            if want is not None:
+                return out if want == np.dtype(np.int64) else out.to(torch_dtype(want))
+        # not numpy-callable: elementwise results return to the record type
+        return out.to(orig) if tuple(out.shape) == record_shape(tuple(args)) else out
     return wrapped
 
 

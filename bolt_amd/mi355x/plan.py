@@ -564,6 +564,50 @@ def swap_perm(ndim, split, kaxes, vaxes):
     return perm, split - len(K) + len(V)
 
 
+def swap_shape(shape, split, kaxes, vaxes):
+    """Shape and split BoltArraySpark.swap reports (array.py:758-763), or None
+    where the reference's chain raises.
+
+    The swap is chunk -> keys_to_values(K) -> values_to_keys(V + #K) ->
+    unchunk, and three of those steps drop or add a unit value axis:
+      * chunk of an all-key array appends a (1,) value axis (chunk.py:113-118);
+      * keys_to_values of records whose values are (1,) drops that axis
+        (chunk.py:284-287);
+      * values_to_keys down to no value axes appends (1,) (chunk.py:342-345);
+      * unchunk of records whose values are (1,) drops it (chunk.py:193-197).
+    So a swap whose values end as one axis of length 1 (a (1, 5) swap((0,),
+    (0,)) -> (5,)) or that moves keys next to a lone (1,) value axis loses
+    that axis.  The bytes are x.transpose(swap_perm) either way: only unit
+    axes differ.  None where the reference's chain raises IndexError
+    (values_to_keys' mask indexes past the values left after the
+    keys_to_values squeeze, chunk.py:293, or no longer fits records that
+    squeeze cut short, chunk.py:329); the caller keeps numpy's shape there.
+    """
+    K = sorted(set(int(k) for k in kaxes))
+    V = sorted(set(int(v) for v in vaxes))
+    kshape = [int(d) for d in shape[:split]]
+    vshape = [int(d) for d in shape[split:]] or [1]
+    if K:
+        squeeze = vshape == [1]
+        if squeeze and any(kshape[k] == 1 for k in K):
+            # numpy's squeeze drops the moved unit key's label axis from every
+            # record too, and values_to_keys' mask no longer fits the records
+            # (chunk.py:329, IndexError in the reference)
+            return None
+        vshape = [kshape[k] for k in K] + vshape
+        kshape = [d for i, d in enumerate(kshape) if i not in K]
+        if squeeze:
+            vshape = vshape[:-1]
+    Vn = [v + len(K) for v in V]
+    if any(v >= len(vshape) for v in Vn):
+        return None
+    kshape = kshape + [vshape[v] for v in Vn]
+    vshape = [d for i, d in enumerate(vshape) if i not in Vn] or [1]
+    if vshape == [1]:
+        vshape = []
+    return tuple(kshape + vshape), len(kshape)
+
+
 def transpose_split(p, split):
     """Decomposition of BoltArraySpark.transpose (array.py:788-806).
 

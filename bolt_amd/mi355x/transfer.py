@@ -109,37 +109,44 @@ def staging_buffers():
     return [torch.empty(CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
 
 
-def copy_to_host(t, out, staging=None):
+def copy_to_host(t, out, staging=None, produce=None, chunk=CHUNK):
     """out[:] = the bytes of uint8 tensor ``t`` (``out`` a host uint8 ndarray of
     t.numel() bytes), staged through two page-locked chunks (``staging``, or
     two from torch's caching host allocator): the host copy out of chunk i
-    overlaps the DMA of chunk i+1."""
+    overlaps the DMA of chunk i+1.
+
+    ``produce(lo, hi, k)``, when given, replaces ``t`` (pass its device): it
+    queues on the current stream whatever fills bytes [lo, hi) of the result
+    into device window ``k`` (0 or 1, alternating) and returns that window's
+    tensor -- a row-padded array's rows compacted window by window
+    (array.py ``_padded_to_host``); ``chunk`` is then the window size."""
     import torch
-    n = t.numel()
+    n = out.size if produce is not None else t.numel()
     if n == 0:
         return
     if t.device.type != "cuda":
-        out[:] = t.numpy()
+        out[:] = (produce(0, n, 0) if produce is not None else t).numpy()
         return
     stream = torch.cuda.current_stream(t.device)
+    src = (lambda lo, hi, k: produce(lo, hi, k)) if produce is not None else (lambda lo, hi, k: t[lo:hi])
     if n <= SMALL:
         host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-        host.copy_(t, non_blocking=True)
+        host.copy_(src(0, n, 0), non_blocking=True)
         stream.synchronize()
         _par_copy(out, host.numpy())
         return
     bufs = staging if staging is not None else staging_buffers()
     evs = [torch.cuda.Event(), torch.cuda.Event()]
-    starts = list(range(0, n, CHUNK))
+    starts = list(range(0, n, chunk))
     # keep one DMA in flight ahead of the host copy out of the previous chunk
     for i, lo in enumerate(starts):
-        hi = min(n, lo + CHUNK)
+        hi = min(n, lo + chunk)
         k = i % 2
-        bufs[k][:hi - lo].copy_(t[lo:hi], non_blocking=True)
+        bufs[k][:hi - lo].copy_(src(lo, hi, k), non_blocking=True)
         evs[k].record(stream)
         if i > 0:
             plo = starts[i - 1]
-            phi = min(n, plo + CHUNK)
+            phi = min(n, plo + chunk)
             evs[1 - k].synchronize()
             _par_copy(out[plo:phi], bufs[1 - k].numpy()[:phi - plo])
     lo = starts[-1]

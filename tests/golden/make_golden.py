@@ -800,11 +800,59 @@ def gen_reduce():
                             add(case, out=a)
 
 
+def gen_unit_axes():
+    """Swaps and statistics around length-1 axes (round 6): the reference's swap
+    chain squeezes unit value axes (chunk.py:193-197, :284-287, :342-345), so a
+    (1, 5) swap((0,), (0,)) is (5,) and statistics whose _align swaps end on
+    (1,) values are scalars (array.py:85-115, :316-329).  Only cases the
+    reference answers are kept (a chain that raises in the reference keeps
+    numpy's answer in bolt_amd, docs/HISTORY.md §4 item 6), and only those
+    whose result is not numpy's shape."""
+    swaps = [((1, 5), (0,), (0,), (0,)), ((5, 3, 1), (0,), (), (0,)), ((2, 3, 1), (0, 1), (1,), ()),
+             ((2, 2, 5, 1), (0, 1, 2), (1, 2), ()), ((5, 1), (0,), (0,), (0,)), ((3, 4, 1, 1), (0,), (), (0, 1)),
+             ((6, 1, 1), (0,), (0,), (1,)), ((1, 1), (0,), (0,), (0,)), ((4, 6, 1), (0,), (0,), (1,)),
+             ((3, 2, 4, 1), (0, 1), (0,), (1,)), ((2, 3, 4, 1), (0, 1, 2), (0, 2), ())]
+    for i, (sh, axis, kax, vax) in enumerate(swaps):
+        s = spec(sh, ("float32", "float64", "int16", "uint8")[i % 4], "normal" if i % 4 < 2 else "ints", 30 + i)
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=axis)
+        case = {"op": "swap", "input": s, "axis": list(axis), "kaxes": list(kax), "vaxes": list(vax), "size": "150"}
+        r = run(lambda: b.swap(kax, vax), case)
+        if r is None:
+            continue
+        case.update(shape=list(r.shape), split=r.split)
+        add(case, out=_sorted_array(r))
+    shapes = [((3, 4, 1), (0, 1)), ((4, 1), (0,)), ((1, 5), (0,)), ((2, 3, 1, 1), (0, 1)), ((5, 2, 1), (0,)),
+              ((1, 3, 1, 2, 1), (0, 1)), ((3, 1, 4), (0, 1, 2)), ((2, 1, 1, 3), (0,))]
+    for i, (sh, kaxis) in enumerate(shapes):
+        s = spec(sh, ("float64", "float32", "int32", "uint16")[i % 4], "normal" if i % 4 < 2 else "ints", 50 + i)
+        x = make_input(s)
+        b = bolt.array(x, sc, axis=kaxis, npartitions=2)
+        nd = x.ndim
+        axes = [(a,) for a in range(nd)] + [(a, c) for a in range(nd) for c in range(a + 1, nd)]
+        for ax in axes:
+            for name in ("mean", "var", "std", "sum", "max"):
+                for keep in (False, True):
+                    case = {"op": "stat", "input": s, "axis": list(kaxis), "npartitions": 2,
+                            "name": name, "reduce_axis": list(ax), "keepdims": keep}
+                    r = run(lambda: getattr(b, name)(axis=ax, keepdims=keep), case)
+                    if r is None:
+                        continue
+                    a = np.asarray(r.toarray() if hasattr(r, "toarray") else r)
+                    kept = tuple(d for j, d in enumerate(sh) if j not in ax)
+                    plain = tuple(1 if j in ax else d for j, d in enumerate(sh)) if keep else kept
+                    if a.shape == plain or (plain == (1,) and a.shape == ()):
+                        continue  # numpy's shape: covered elsewhere
+                    case["result_type"] = type(r).__name__
+                    case["result_dtype"] = str(a.dtype)
+                    add(case, out=a)
+
+
 if __name__ == "__main__":
     sc = FakeContext(2)
     for g in (gen_construct, gen_swap, gen_transpose, gen_chunk, gen_moves, gen_getplan, gen_stats,
               gen_stat_errors, gen_getitem, gen_concatenate, gen_chunk_map,
-              gen_functional, gen_stats_numerics, gen_reshape, gen_reduce):
+              gen_functional, gen_stats_numerics, gen_reshape, gen_reduce, gen_unit_axes):
         try:
             g()
         except Exception:

@@ -14,6 +14,7 @@ test executor and (marker `gpu`) on the HIP kernels.
 import os
 
 import numpy as np
+import torch
 import pytest
 
 import bolt_amd as bolt
@@ -23,7 +24,7 @@ from oracle import bolt_oracle as O
 NCASES = 200
 # a soak run takes other seeds: BOLT_AMD_FUZZ_SEEDS=start:stop (default 0:NCASES)
 _SEEDS = range(*[int(v) for v in os.environ.get("BOLT_AMD_FUZZ_SEEDS", "0:%d" % NCASES).split(":")])
-DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16, np.uint16]
+DTYPES = [np.float32, np.float64, np.int32, np.uint8, np.int16, np.uint16, np.uint32]
 
 
 def _factor(rng, n, parts):
@@ -47,18 +48,12 @@ def _check_array(got, want):
     assert _same(got.toarray(), O.toarray(want))
 
 
-def _check_swapped(got, want, cast=False):
+def _check_swapped(got, want):
     """A result built through the reference's swap (map / filter align their
-    axes with one): its shape, or -- where the reference's swap loses a
-    length-1 value axis (a reference bug not kept, docs/HISTORY.md §4 item 6)
-    -- the same shape up to that unit axis; the same bytes either way."""
-    if got.shape != tuple(want.shape):
-        assert [d for d in got.shape if d != 1] == [d for d in want.shape if d != 1], (got.shape, want.shape)
-    else:
-        assert got.split == want.split, (got.split, want.split)
-    w = O.toarray(want)
-    a = got.toarray()
-    assert a.tobytes() == (w.astype(a.dtype) if cast else w).tobytes()
+    axes with one): its shape and split (unit-axis squeezes included), dtype
+    and bytes."""
+    assert got.shape == tuple(want.shape) and got.split == want.split, (got.shape, want.shape, got.split, want.split)
+    assert _same(got.toarray(), O.toarray(want))
 
 
 def _mask_bug(e):
@@ -175,7 +170,18 @@ def test_api_fuzz(bctx, seed):
     fn = (lambda v: v * 2 + 1)
     want, got = _raises_like(lambda: O.map_(rs, fn, axis=max_ax), lambda: b.map(fn, axis=max_ax))
     if want is not None:
-        _check_swapped(got, want, cast=True)
+        _check_swapped(got, want)
+    if np.dtype(dtype) in (np.dtype(np.uint16), np.dtype(np.uint32)):
+        # records torch has no arithmetic for (functional.user_fn): a record sum
+        # is numpy's uint64 and exact past 2**32, an explicit cast is kept
+        big = x.astype(np.uint64) * 0 + (np.iinfo(dtype).max - int(rng.integers(0, 5)))
+        bb, rb = bolt.array(big.astype(dtype), bctx, axis=axis), O.parallelize(big.astype(dtype), axis=axis)
+        for f in (lambda v: v.sum(),
+                  lambda v: v.to(torch.int64) if hasattr(v, "to") else v.astype(np.int64),
+                  lambda v: (v.to(torch.int64) if hasattr(v, "to") else v.astype(np.int64)) * 3):
+            want, got = _raises_like(lambda: O.map_(rb, f, axis=max_ax), lambda: bb.map(f, axis=max_ax))
+            if want is not None:
+                _check_swapped(got, want)
 
     # filter (array.py:193-241): keep records whose sum is above the median
     fax = tuple(sorted(rng.choice(nd, int(rng.integers(1, nd + 1)), replace=False).tolist()))

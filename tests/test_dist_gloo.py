@@ -89,7 +89,10 @@ def _body(rank, world, device="cpu"):
     for shp in ((world + 1, 6, 10), (2 * world + 1, 5, 7), (world - 1 or 1, 9, 8)):
         u = (np.arange(int(np.prod(shp))) % 1009).astype(np.float32).reshape(shp)
         bu = bolt.array(u, ctx)
-        assert _exact(bu.swap((0,), (0, 1)).toarray(), u.transpose(1, 2, 0)), shp
+        want = u.transpose(1, 2, 0)
+        if want.shape[-1] == 1:  # a lone (1,) value axis: the reference's unchunk squeezes it
+            want = want.reshape(want.shape[:-1])
+        assert _exact(bu.swap((0,), (0, 1)).toarray(), want), shp
         assert _exact(bu.transpose(2, 0, 1).toarray(), u.transpose(2, 0, 1)), shp
     bdist.STAGE_BYTES = None
     assert _exact(ba.keys.transpose((1, 0)).toarray(), a.transpose(1, 0, 2, 3))

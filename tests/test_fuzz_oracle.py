@@ -49,7 +49,7 @@ def _records_equal(got, want):
     assert len(got) == len(want)
     for (gk, gv), (wk, wv) in zip(got, want):
         assert gk == tuple(wk), (gk, wk)
-        assert _exact(gv, np.ascontiguousarray(wv)), gk
+        assert _exact(gv, np.ascontiguousarray(wv) if np.ndim(wv) else np.asarray(wv)), gk
 
 
 @pytest.mark.parametrize("seed", _SEEDS)
@@ -131,18 +131,69 @@ def check_case(bctx, seed):
 
 def test_swap_length1_value_axis(bctx):
     """A swap whose result has exactly one value axis of length 1: the reference's
-    unchunk squeezes it (chunk.py:193-197, meant for the all-keys singleton), so
-    its (5, 3, 1) swap((), (0,)) is (5, 3) with split 2.  bolt_amd keeps the axis
-    (numpy's transpose); transposes through such shapes raise IndexError in the
-    reference and succeed here."""
+    unchunk squeezes it (chunk.py:193-197), so its (5, 3, 1) swap((), (0,)) is
+    (5, 3) with split 2 and its (1, 5) swap((0,), (0,)) is (5,) -- bolt_amd
+    returns the same shapes (plan.swap_shape); the bytes are numpy's transpose.
+    A transpose through such shapes raises in the reference and is numpy's
+    here (docs/HISTORY.md §4 item 6)."""
     x = np.arange(15, dtype=np.float32).reshape(5, 3, 1)
     b = bolt.array(x, bctx)
     s = b.swap((), (0,))
     ws = O.swap(O.parallelize(x), (), (0,))
     assert ws.shape == (5, 3) and ws.split == 2          # the reference (oracle pinned to it)
-    assert s.shape == (5, 3, 1) and s.split == 2         # bolt_amd
-    assert _exact(s.toarray().reshape(5, 3), O.toarray(ws))
+    assert s.shape == (5, 3) and s.split == 2
+    assert _exact(s.toarray(), O.toarray(ws))
+    y = np.arange(5.).reshape(1, 5)
+    s = bolt.array(y, bctx).swap((0,), (0,))
+    assert s.shape == (5,) and s.split == 1 and _exact(s.toarray(), y.reshape(5))
     assert _exact(bolt.array(np.zeros((3, 1)), bctx).T.toarray(), np.zeros((1, 3)))
+
+
+def _raises(f):
+    try:
+        return f(), None
+    except Exception as e:  # noqa: BLE001 -- the oracle's refusal, whatever its type
+        return None, e
+
+
+@pytest.mark.parametrize("seed", range(150))
+def test_unit_axes_against_oracle(bctx, seed):
+    """Arrays with length-1 axes through swap and the statistics: wherever the
+    oracle (the reference's chain restated) answers, bolt_amd's shape, split and
+    values are its; where it raises, bolt_amd is numpy's (not checked here)."""
+    rng = np.random.default_rng(7000 + seed)
+    ndim = int(rng.integers(2, 5))
+    shape = tuple(int(rng.choice([1, 1, 2, 3, 4])) for _ in range(ndim))
+    split = int(rng.integers(1, ndim + 1))
+    x = (3 + rng.standard_normal(shape)).astype([np.float32, np.float64][seed % 2])
+    axis = tuple(range(split))
+    b = bolt.array(x, bctx, axis=axis)
+    rs = O.parallelize(x, axis=axis, npartitions=2)
+    for _ in range(3):
+        kax = tuple(sorted(rng.choice(split, int(rng.integers(0, split + 1)), replace=False).tolist()))
+        vax = tuple(sorted(rng.choice(ndim - split, int(rng.integers(0, ndim - split + 1)),
+                                      replace=False).tolist()))
+        if (len(kax) == split and not vax) or not (kax or vax):
+            continue
+        ws, err = _raises(lambda: O.swap(rs, kax, vax))
+        if err is None:
+            ws_arr, err = _raises(lambda: O.toarray(ws))
+        if err is not None:
+            continue
+        s = b.swap(kax, vax)
+        assert s.shape == ws.shape and s.split == ws.split, (kax, vax, s.shape, ws.shape)
+        assert _exact(s.toarray(), ws_arr)
+    for name, oname in (("mean", "mean"), ("var", "variance"), ("std", "stdev")):
+        ax = tuple(sorted(rng.choice(ndim, int(rng.integers(1, ndim + 1)), replace=False).tolist()))
+        keep = bool(rng.random() < 0.5)
+        want, err = _raises(lambda: O.stat(rs, oname, axis=ax, keepdims=keep))
+        if err is not None:
+            continue
+        got = getattr(b, name)(axis=ax, keepdims=keep)
+        ga, wa = np.asarray(got), np.asarray(want)
+        assert ga.shape == wa.shape and ga.dtype == wa.dtype, (name, ax, keep, ga.shape, wa.shape)
+        tol = 1e-5 if ga.dtype == np.float32 else 1e-12
+        assert np.allclose(ga, wa, rtol=tol, atol=tol, equal_nan=True), (name, ax)
 
 
 def test_transpose_all_key_array(bctx):

@@ -5,6 +5,12 @@ on bolt_amd's CPU executor of the kernel contracts, in a child process, and
 must report no difference beyond the reference bugs docs/HISTORY.md §4 lists.
 Skipped where the reference is absent (the GPU box); nothing from it is copied
 or shipped.  (profiles/r05p_reference_diff_fuzz.txt: 12,000 seeds.)
+
+The second test draws length-1 axes too (BOLT_AMD_DIFF_MIN_EXTENT=1): every
+result the reference returns must have its shape and split (its swap chain
+squeezes unit value axes, plan.swap_shape); where the reference raises and
+numpy has an answer, bolt_amd's numpy answer is counted, not failed
+(profiles/r06a_reference_diff_unit_axes.txt).
 """
 import os
 import subprocess
@@ -20,6 +26,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_random_chains_match_the_reference(tmp_path):
     env = dict(os.environ)
     env["PYTHONDONTWRITEBYTECODE"] = "1"  # the reference tree is read-only
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "reference_diff_fuzz.py"), "0", "1500"],
+                       env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "seeds 0..1499: 0 failed" in out, out[-4000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "bolt", "spark")), reason="reference not present")
+def test_random_chains_with_unit_axes_match_the_reference(tmp_path):
+    env = dict(os.environ)
+    env["PYTHONDONTWRITEBYTECODE"] = "1"
+    env["BOLT_AMD_DIFF_MIN_EXTENT"] = "1"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "reference_diff_fuzz.py"), "0", "1500"],
                        env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=900)
     out = r.stdout + r.stderr

@@ -330,3 +330,37 @@ def test_gpu_reduce_rows_abi(gpu_ctx, dtype):
                 assert a.cpu().numpy().view(odt).tobytes() == x[:, :R].max(axis=1).tobytes()
     with pytest.raises(_lib.BoltDeviceError, match="row_pitch"):
         be.reduce_rows(_lib.STAT_SUM, padded, dtype_code(np.dtype(dtype)), 4, 10, 9, a, dtype_code(np.dtype(dtype)))
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_toarray_reads_padded_rows(bctx, small_pitch, monkeypatch, case):
+    """toarray / records of a padded result compact window by window into the
+    host result (array.py _padded_to_host): the array stays padded and no dense
+    device copy is made."""
+    shape, kax, vax, dtype = CASES[case]
+    x = _data(shape, dtype, 200 + case)
+    axis = tuple(range(len(kax)))
+    s = bolt.array(x, bctx, axis=axis).swap(kax, vax)
+    assert _padded(s)
+    got = s.toarray()
+    assert _padded(s) and "_data" not in s.__dict__
+    monkeypatch.setattr(A, "ROW_PITCH", False)
+    want = bolt.array(x, bctx, axis=axis).swap(kax, vax).toarray()
+    assert got.shape == want.shape and got.dtype == want.dtype and got.tobytes() == want.tobytes()
+    recs = list(s.records())
+    assert _padded(s) and len(recs) == int(np.prod(s.shape[:s.split]))
+
+
+@pytest.mark.gpu
+def test_gpu_padded_toarray_windows(gpu_ctx, monkeypatch):
+    """A padded swap result larger than one egress window (transfer.CHUNK, set
+    to 8 MiB here: 33 windows) goes to the host window by window, bit-exact,
+    with the array still padded afterwards."""
+    from bolt_amd.mi355x import transfer
+    monkeypatch.setattr(transfer, "CHUNK", 8 << 20)
+    x = (np.arange(500 * 256 * 512, dtype=np.int64) % 65521).astype(np.float32).reshape(500, 256, 512)
+    s = bolt.array(x, gpu_ctx).swap((0,), (0, 1))
+    assert _padded(s) and s.__dict__["_pitch"] == 512      # 2000-B rows at 2048 B
+    got = s.toarray()
+    assert _padded(s) and "_data" not in s.__dict__
+    assert got.shape == (256, 512, 500) and got.tobytes() == np.ascontiguousarray(x.transpose(1, 2, 0)).tobytes()

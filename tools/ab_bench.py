@@ -26,6 +26,10 @@ def load(path):
     lib.bm_reduce.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                               ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                               ctypes.c_size_t, ctypes.c_void_p]
+    if hasattr(lib, "bm_reduce_rows"):
+        lib.bm_reduce_rows.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_void_p]
     lib.bm_reduce_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                               ctypes.c_int64, ctypes.POINTER(ctypes.c_size_t)]
     lib.bm_record_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
@@ -97,6 +101,23 @@ class Reduce(object):
         rc = lib.bm_reduce(self.stat, ctypes.c_void_p(self.src.data_ptr()), self.code, self.O, self.R, self.I,
                            ctypes.c_void_p(self.out.data_ptr()), self.ocode,
                            ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(), stream())
+        assert rc == 0, lib.bm_last_error()
+
+
+class ReduceRows(Reduce):
+    """bm_reduce_rows: O rows of R elements at a pitch of P elements (the
+    statistics of a row-padded swap result: C2 is 262144 rows of 2000 float32
+    at 2048)."""
+
+    def __init__(self, stat, O, R, P, dtype, out_dtype):
+        Reduce.__init__(self, stat, O, P, 1, dtype, out_dtype)
+        self.R, self.P = R, P
+        self.bytes = O * R * np.dtype(dtype).itemsize + self.out.numel()
+
+    def __call__(self, lib):
+        rc = lib.bm_reduce_rows(self.stat, ctypes.c_void_p(self.src.data_ptr()), self.code, self.O, self.R, self.P,
+                                ctypes.c_void_p(self.out.data_ptr()), self.ocode,
+                                ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(), stream())
         assert rc == 0, lib.bm_last_error()
 
 
@@ -309,6 +330,14 @@ OPS = {
     "c2_swap": lambda: Permute((2000, 512 * 512), (1, 0), np.float32),
     "c2_mean_rows": lambda: Reduce(0, 512 * 512, 2000, 1, np.float32, np.float32),
     "c2_std_rows": lambda: Reduce(2, 512 * 512, 2000, 1, np.float32, np.float32),
+    "c2_sum_rows": lambda: Reduce(3, 512 * 512, 2000, 1, np.float32, np.float32),
+    "c2_max_rows": lambda: Reduce(4, 512 * 512, 2000, 1, np.float32, np.float32),
+    "c2_mean_prow": lambda: ReduceRows(0, 512 * 512, 2000, 2048, np.float32, np.float32),
+    "c2_std_prow": lambda: ReduceRows(2, 512 * 512, 2000, 2048, np.float32, np.float32),
+    "c2_sum_prow": lambda: ReduceRows(3, 512 * 512, 2000, 2048, np.float32, np.float32),
+    "c2_max_prow": lambda: ReduceRows(4, 512 * 512, 2000, 2048, np.float32, np.float32),
+    "c2q_mean_prow": lambda: ReduceRows(0, 128 * 512, 2000, 2048, np.float32, np.float32),
+    "c2q_std_prow": lambda: ReduceRows(2, 128 * 512, 2000, 2048, np.float32, np.float32),
     "c2_mean_cols": lambda: Reduce(0, 1, 2000, 512 * 512, np.float32, np.float32),
     "c2_std_cols": lambda: Reduce(2, 1, 2000, 512 * 512, np.float32, np.float32),
     "c3_swap": lambda: Permute((1024, 256, 256, 32), (1, 2, 0, 3), np.float32),
