@@ -703,64 +703,37 @@ __global__ void __launch_bounds__(kThreads)
   // var / std: every value is shifted by the row's first element P (shared
   // by all chunks of the row), so the Welford means stay near zero and keep
   // their digits on offset data (1e6 + N(0,1)); batches bound outliers.
-  //
-  // The pivots are lane 0's first element.  Where lane 0 runs the main loop,
-  // its first load is peeled and the pivot broadcast from it: a separate
-  // element load of the row's first line would be a second HBM read of it
-  // (that load is temporal, the vector loads non-temporal).
-  double P = 0.0;
-  T v[kRowsUnroll][VEC];
-  const bool peel = (MODE == M_MEAN || MODE == M_MOM) &&
-                    r_lo + VEC + (int64_t)(kRowsUnroll - 1) * stride <= r_hi;
-  bool have = false;
-  if (peel) {
-    if (j + VEC + (kRowsUnroll - 1) * stride <= r_hi) {
+  if (MODE == M_MEAN) acc.pivot(to_f64(row[r_lo]));
+  const double P = (MODE == M_MOM) ? to_f64(row[0]) : 0.0;
+  // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
+  for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
+    T v[kRowsUnroll][VEC];
 #pragma unroll
-      for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
-      have = true;
-    }
-    const double first = __shfl(have ? to_f64(v[0][0]) : 0.0, 0, 64);
-    if (MODE == M_MEAN) acc.pivot(first);
-    if (MODE == M_MOM) P = (r_lo == 0) ? first : to_f64(row[0]);
-  } else {
-    if (MODE == M_MEAN) acc.pivot(to_f64(row[r_lo]));
-    if (MODE == M_MOM) P = to_f64(row[0]);
-  }
-  auto consume = [&](T (&vv)[kRowsUnroll][VEC]) {
+    for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
     if constexpr (MODE == M_MOM) {
       // the kRowsUnroll * VEC values in hand form one Welford batch
       double x[kRowsUnroll * VEC];
 #pragma unroll
       for (int u = 0; u < kRowsUnroll; ++u)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) x[u * VEC + k] = to_f64(vv[u][k]);
+        for (int k = 0; k < VEC; ++k) x[u * VEC + k] = to_f64(v[u][k]);
       w.add_main<kRowsUnroll * VEC>(x, P);
-      return;
+      continue;
     }
 #pragma unroll
     for (int u = 0; u < kRowsUnroll; ++u) {
       if constexpr (MODE == M_MEAN && VEC % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < VEC; k += 2) acc.add2(to_f64(vv[u][k]), to_f64(vv[u][k + 1]));
+        for (int k = 0; k < VEC; k += 2) acc.add2(to_f64(v[u][k]), to_f64(v[u][k + 1]));
         continue;
       }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (MODE == M_MEAN) acc.add(to_f64(vv[u][k]));
-        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(vv[u][k]));
-        else us = bop<T, MODE>(us, belem<T, MODE>(vv[u][k]));
+        if (MODE == M_MEAN) acc.add(to_f64(v[u][k]));
+        else if (facc_mode<MODE>()) fs = fop<MODE>(fs, to_f64(v[u][k]));
+        else us = bop<T, MODE>(us, belem<T, MODE>(v[u][k]));
       }
     }
-  };
-  if (have) {
-    consume(v);
-    j += kRowsUnroll * stride;
-  }
-  // kRowsUnroll 16-B vectors in flight per lane (HBM latency cover)
-  for (; j + VEC + (kRowsUnroll - 1) * stride <= r_hi; j += kRowsUnroll * stride) {
-#pragma unroll
-    for (int u = 0; u < kRowsUnroll; ++u) vload_nt<T, VEC>(row + j + u * stride, v[u]);
-    consume(v);
   }
   // var / std: the rest of the row and the cross-lane merge run as sums
   // around one wave-wide pivot C = lane 0's Welford mean (lane 0 holds 1/64

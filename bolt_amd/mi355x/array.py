@@ -28,7 +28,7 @@ from bolt_amd.mi355x.context import local_shape
 from bolt_amd.mi355x.dist import all_gather_bytes, concat_rows_sharded, gather_to_host, permute_sharded, redistribute_rows, select_sharded, _empty
 from bolt_amd.mi355x.transfer import finish_host_result, host_result, to_device, to_host
 from bolt_amd.local import BoltArrayLocal
-from bolt_amd.mi355x.plan import getplan, check_plan, swap_perm, swap_shape, reduce_layout, stat_dtype
+from bolt_amd.mi355x.plan import getplan, check_plan, padded_strides, swap_perm, swap_shape, reduce_layout, stat_dtype
 from bolt_amd.utils import tupleize, argpack, inshape, istransposeable, isreshapeable
 
 _STAT_CODES = {'mean': _lib.STAT_MEAN, 'variance': _lib.STAT_VAR, 'stdev': _lib.STAT_STD}
@@ -185,15 +185,7 @@ def _pitch_fits(pp, es, device):
     return need <= free
 
 
-def _padded_strides(shape, P):
-    """C-order element strides of ``shape`` with rows (the last axis) P elements apart."""
-    nd = len(shape)
-    st = [1] * nd
-    if nd >= 2:
-        st[nd - 2] = P
-        for k in range(nd - 3, -1, -1):
-            st[k] = st[k + 1] * shape[k + 1]
-    return st
+_padded_strides = padded_strides
 
 
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
@@ -335,9 +327,10 @@ class BoltArrayMI355X(BoltArray):
         pbuf, P = d["_pbuf"], d["_pitch"]
         es = self._dtype.itemsize
         R = self._shape[-1]
-        rows = int(np.prod(self._shape[:-1], dtype=np.int64))
+        rows = int(np.prod(self._local_shape[:-1], dtype=np.int64))
         data = _empty(rows * R * es, pbuf.device)
-        backend_for(pbuf.device).copy_strided(pbuf, 0, data, 0, [rows, R], [P, 1], [R, 1], es)
+        if rows and R:
+            backend_for(pbuf.device).copy_strided(pbuf, 0, data, 0, [rows, R], [P, 1], [R, 1], es)
         d["_data"] = data
         del d["_pbuf"], d["_pitch"]
         return data
@@ -430,16 +423,8 @@ class BoltArrayMI355X(BoltArray):
             data = self._data
         elif ROW_PITCH and self._ctx.world_size == 1:
             es = self._dtype.itemsize
-            key = (mv, es)
-            pp = _PITCH_PLANS.get(key, False)
-            if pp is False:
-                pp = _pitch_plan(mv, self._shape, es)
-                if len(_PITCH_PLANS) > 4096:
-                    _PITCH_PLANS.clear()
-                _PITCH_PLANS[key] = pp
+            pp = self._pitch_of(mv, es)
             d = self.__dict__
-            if pp is not None and not _pitch_fits(pp, es, self._device):
-                pp = None
             if "_pbuf" in d:
                 # a padded source is read in place: its strides, permuted
                 src, pstr = d["_pbuf"], _padded_strides(self._shape, d["_pitch"])
@@ -459,9 +444,32 @@ class BoltArrayMI355X(BoltArray):
                 data = _empty(n * es, src.device)
                 be.copy_strided(src, 0, data, 0, list(new_shape), sstr, _padded_strides(new_shape, new_shape[-1]), es)
         else:
-            data = permute_sharded(self._ctx, backend_for(self._data.device), self._data, self._shape, perm,
-                                   self._dtype.itemsize)
+            # across GPUs: the exchange's pack reads a padded source in place
+            # and its unpack writes the result's rows at the same pitch rule
+            # as on one GPU
+            es = self._dtype.itemsize
+            pp = self._pitch_of(mv, es) if ROW_PITCH else None
+            d = self.__dict__
+            src = d["_pbuf"] if "_pbuf" in d else self._data
+            data = permute_sharded(self._ctx, backend_for(src.device), src, self._shape, perm, es,
+                                   src_pitch=d.get("_pitch"), out_pitch=None if pp is None else pp[0])
+            if pp is not None:
+                return self._derive_padded(data, pp[0], new_shape, split)
         return self._derive(data, new_shape, split)
+
+    def _pitch_of(self, mv, es):
+        """The pitched copy plan of move ``mv`` (cached, see _pitch_plan), or
+        None when the result stays dense or the device lacks room for it."""
+        key = (mv, es)
+        pp = _PITCH_PLANS.get(key, False)
+        if pp is False:
+            pp = _pitch_plan(mv, self._shape, es)
+            if len(_PITCH_PLANS) > 4096:
+                _PITCH_PLANS.clear()
+            _PITCH_PLANS[key] = pp
+        if pp is not None and not _pitch_fits(pp, es, self._device):
+            return None
+        return pp
 
     def chunk(self, size="150", axis=None, padding=None):
         """Chunk the values of every record (array.py:678-714) -> ChunkedArrayMI355X."""
@@ -875,7 +883,7 @@ class BoltArrayMI355X(BoltArray):
             newshape = list(self._shape)
             newshape[loc] = len(idx)
             d = self.__dict__
-            if "_pbuf" in d:
+            if "_pbuf" in d and self._ctx.world_size == 1:
                 # padded rows (one GPU): taking along the last axis gathers
                 # within the rows (a dense result); along another axis whole
                 # padded rows move and the result keeps the pitch
@@ -973,7 +981,8 @@ class BoltArrayMI355X(BoltArray):
         shape = tuple(d for i, d in enumerate(self._shape) if i not in drop)
         split = len([d for d in range(self._split) if d not in drop])
         d = self.__dict__
-        if "_pbuf" in d and len(shape) >= 2 and (self.ndim - 1) not in drop:
+        if "_pbuf" in d and len(shape) >= 2 and (self.ndim - 1) not in drop and \
+                (0 not in drop or self._ctx.world_size == 1):
             # unit axes only: a padded array's rows stay as they are
             return self._derive_padded(d["_pbuf"], d["_pitch"], shape, split)
         data = self._data
@@ -1018,7 +1027,18 @@ class BoltArrayMI355X(BoltArray):
             _REDUCE_PLANS[pkey] = plan
         axset, kept, out_shape, out_dtype, code, ocode, perm, O, R, I, nloc, loc_out, nout = plan
         pbuf = self.__dict__.get("_pbuf")
-        if pbuf is not None and perm is None and I == 1 and R == lshape[-1] and nloc:
+        if pbuf is not None and perm is None and I == 1 and R == lshape[-1] and ctx.world_size > 1 \
+                and 0 not in axset:
+            # last-axis statistic of a row-padded slab: every output is this
+            # rank's, read in place, then gathered like the dense path's
+            be = backend_for(pbuf.device)
+            out = _empty(nout * out_dtype.itemsize, pbuf.device)
+            if nout and nloc:
+                be.reduce_rows(stat, pbuf, code, O, R, self._pitch, out, ocode)
+            sizes = [int(np.prod((hi - lo,) + out_shape[1:], dtype=np.int64)) * out_dtype.itemsize
+                     for lo, hi in ctx.bounds(self._shape[0])]
+            return to_host(all_gather_bytes(ctx, out, sizes), out_dtype, out_shape), out_dtype
+        if pbuf is not None and perm is None and I == 1 and R == lshape[-1] and nloc and ctx.world_size == 1:
             # last-axis statistic of a row-padded array: read the rows in place
             be = backend_for(pbuf.device)
             host = host_result(be, nout * out_dtype.itemsize, pbuf.device)
@@ -1028,7 +1048,7 @@ class BoltArrayMI355X(BoltArray):
             out = _empty(nout * out_dtype.itemsize, pbuf.device)
             be.reduce_rows(stat, pbuf, code, O, R, self._pitch, out, ocode)
             return to_host(out, out_dtype, out_shape), out_dtype
-        if pbuf is not None and perm is None and I > 1 and I % lshape[-1] == 0 and nloc:
+        if pbuf is not None and perm is None and I > 1 and I % lshape[-1] == 0 and nloc and ctx.world_size == 1:
             # leading / middle axes of a row-padded array: the columns run over
             # the padded rows as if the last axis were P long; every column is
             # its own reduction, so the pad columns' (unwritten) values reach
@@ -1297,13 +1317,19 @@ class BoltArrayMI355X(BoltArray):
         slabs are gathered window by window (dist.gather_to_host): device
         memory per rank stays at its slab plus one window."""
         ctx = self._ctx
-        if "_pbuf" in self.__dict__:
+        d = self.__dict__
+        if "_pbuf" in d and ctx.world_size == 1:
             return self._padded_to_host()
         if ctx.world_size == 1:
             return to_host(self._data, self._dtype, self._shape)
         rowbytes = int(np.prod(self._shape[1:], dtype=np.int64)) * self._dtype.itemsize
         rows = self._shape[0] if self._shape else 1  # a 0-d array lives on rank 0
         sizes = [(hi - lo) * rowbytes for lo, hi in ctx.bounds(rows)]
+        if "_pbuf" in d:
+            # padded rows: each egress window compacted on the way
+            es = self._dtype.itemsize
+            spec = (self._shape[-1] * es, d["_pitch"] * es, self._backend)
+            return gather_to_host(ctx, d["_pbuf"], sizes, rows=spec).view(self._dtype).reshape(self._shape)
         return gather_to_host(ctx, self._data, sizes).view(self._dtype).reshape(self._shape)
 
     def _padded_to_host(self):

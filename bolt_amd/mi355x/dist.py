@@ -234,36 +234,53 @@ def egress_window():
     return int(EGRESS_WINDOW) if EGRESS_WINDOW else 2 * transfer.CHUNK
 
 
-def gather_to_host(ctx, local, sizes, out=None):
+def gather_to_host(ctx, local, sizes, out=None, rows=None):
     """The concatenation of every rank's bytes (``sizes[r]`` bytes from rank r,
     in rank order) as a host uint8 ndarray on every rank, gathered window by
-    window (EGRESS_WINDOW).  ``out``: a host uint8 array to fill instead."""
+    window (EGRESS_WINDOW).  ``out``: a host uint8 array to fill instead.
+    ``rows``: (row bytes R*es, pitch bytes P*es, backend) when ``local`` holds
+    row-padded rows: each window's rows are compacted on the way (no dense
+    copy of the slab)."""
     from bolt_amd.mi355x.transfer import copy_to_host
     sizes = [int(v) for v in sizes]
     if out is None:
         out = np.empty(sum(sizes), dtype=np.uint8)
-    if ctx.world_size == 1:
+    if ctx.world_size == 1 and rows is None:
         copy_to_host(local, out)
         return out
-    return gather_windows(ctx, local, sizes, out, all_gather_bytes)
+    return gather_windows(ctx, local, sizes, out, all_gather_bytes, rows)
 
 
-def gather_windows(ctx, local, sizes, out, gather):
+def gather_windows(ctx, local, sizes, out, gather, rows=None):
     """gather_to_host's windows: each window of the global byte sequence is one
     ``gather`` (all_gather_bytes) into a window-sized device buffer, then a
     staged D2H into its place in ``out``; the two page-locked staging buffers
-    are allocated once for all windows."""
+    are allocated once for all windows.  With ``rows`` the windows are whole
+    rows and this rank's piece of each is compacted from its padded rows into
+    one window-sized device buffer first."""
     from bolt_amd.mi355x.transfer import SMALL, copy_to_host, staging_buffers
     total = sum(sizes)
     offs = np.r_[0, np.cumsum(sizes)].astype(np.int64)
     me = ctx.rank
     w = max(1, egress_window())
+    win = None
+    if rows is not None:
+        rb, pb, be = rows
+        w = max(rb, w // rb * rb)  # windows of whole rows (every slab is whole rows too)
+        win = _empty(min(w, max(sizes[me], 0)), local.device) if sizes[me] else None
     staging = staging_buffers() if local.device.type == "cuda" and min(w, total) > SMALL else None
     for g0 in range(0, total, w):
         g1 = min(total, g0 + w)
         part = [max(0, min(g1, int(offs[r + 1])) - max(g0, int(offs[r]))) for r in range(len(sizes))]
         lo = max(g0, int(offs[me])) - int(offs[me])
-        piece = local[lo:lo + part[me]] if part[me] else local[:0]
+        if not part[me]:
+            piece = local[:0]
+        elif rows is None:
+            piece = local[lo:lo + part[me]]
+        else:
+            n = part[me] // rb
+            be.copy_strided(local, (lo // rb) * pb, win, 0, [n, rb], [pb, 1], [rb, 1], 1)
+            piece = win[:part[me]]
         buf = gather(ctx, piece, part)
         copy_to_host(buf, out[g0:g1], staging)
         del buf
@@ -312,13 +329,17 @@ def _test_all_to_all(ctx, send, send_sizes, recv_sizes, unit, async_op):
     return (recv, work) if async_op else recv
 
 
-def permute_sharded(ctx, backend, data, shape, perm, es):
+def permute_sharded(ctx, backend, data, shape, perm, es, src_pitch=None, out_pitch=None):
     """This rank's shard of x.transpose(perm) for a sharded x of global ``shape``.
 
     ``data`` holds this rank's slab of x's leading axis.  Returns the byte
-    tensor of this rank's slab of the result's leading axis.
+    tensor of this rank's slab of the result's leading axis.  ``src_pitch`` /
+    ``out_pitch``: elements between the rows (last axis) of a row-padded
+    source / result (array.py ROW_PITCH); the exchange's pack reads the padded
+    source rows in place and its unpack writes the padded result rows.
     """
-    if ctx.world_size == 1:  # one GPU: one kernel
+    from bolt_amd.mi355x.plan import padded_strides
+    if ctx.world_size == 1 and src_pitch is None and out_pitch is None:  # one GPU: one kernel
         out = _empty(data.numel(), data.device)
         if out.numel():
             backend.permute(data, shape, perm, es, out)
@@ -331,23 +352,27 @@ def permute_sharded(ctx, backend, data, shape, perm, es):
     r = ctx.rank
     in_lo, in_hi = in_b[r]
     loc_in = (in_hi - in_lo,) + shape[1:]
-    sin = contiguous_strides(loc_in)
+    sin = contiguous_strides(loc_in) if src_pitch is None else padded_strides(loc_in, src_pitch)
+    lo, hi = out_b[r]
+    loc_out = (hi - lo,) + out_shape[1:]
+    if out_pitch is None:
+        out = _empty(int(np.prod(loc_out)) * es, data.device)
+        tstr = contiguous_strides(loc_out)
+    else:
+        out = _empty(int(np.prod(loc_out[:-1])) * int(out_pitch) * es, data.device)
+        tstr = padded_strides(loc_out, out_pitch)
 
     if perm[0] == 0 or ctx.world_size == 1:
-        lo, hi = out_b[r]
-        loc_out = (hi - lo,) + out_shape[1:]
-        out = _empty(int(np.prod(loc_out)) * es, data.device)
-        if out.numel():
-            backend.permute(data, loc_in, perm, es, out)
+        if out.numel() and int(np.prod(loc_out)):
+            if src_pitch is None and out_pitch is None:
+                backend.permute(data, loc_in, perm, es, out)
+            else:
+                backend.copy_strided(data, 0, out, 0, list(loc_out), [sin[p] for p in perm], tstr, es)
         return out
 
     a = perm[0]          # input axis that becomes the output's leading axis
     j = perm.index(0)    # where the input's leading axis lands
     G = ctx.world_size
-    lo, hi = out_b[r]
-    loc_out = (hi - lo,) + out_shape[1:]
-    out = _empty(int(np.prod(loc_out)) * es, data.device)
-    tstr = contiguous_strides(loc_out)
     sstr = [sin[p] for p in perm]
     # Pipeline the exchange in K stages: stage k packs its sub-blocks, starts
     # its all-to-all asynchronously (RCCL stream) and, while that runs, the
@@ -469,7 +494,8 @@ def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es, src_
     every destination, the selected rows it holds (they form one run of
     output rows), one all-to-all moves them, and they land in order.
     ``src_strides``: element strides of a source that is not C-contiguous (a
-    row-padded array, one GPU only).
+    row-padded array: plan.padded_strides of the global shape, which are also
+    every slab's).
     """
     shape = tuple(int(x) for x in shape)
     out_shape = tuple(int(x) for x in out_shape)
@@ -484,8 +510,6 @@ def select_sharded(ctx, backend, data, shape, starts, steps, out_shape, es, src_
     mlo, mhi = in_b[r]
     sin = contiguous_strides((mhi - mlo,) + shape[1:])
     if src_strides is not None:
-        if ctx.world_size != 1:
-            raise ValueError("select_sharded: source strides on one GPU only")
         sin = [int(v) for v in src_strides]
     sstr = [sin[k] * steps[k] for k in range(len(shape))]
     inner_off = sum(starts[k] * sin[k] for k in range(1, len(shape)))

@@ -546,6 +546,20 @@ def v2k_copies(old, new, kshape, vmask):
 # swap / transpose  (bolt/spark/array.py)
 # --------------------------------------------------------------------------
 
+def padded_strides(shape, P):
+    """C-order element strides of ``shape`` with rows (the last axis) P elements
+    apart: the layout of a row-padded array (array.py ROW_PITCH).  Only the
+    leading stride depends on the rows' count, not on the leading extent, so
+    the strides of the global shape serve every rank's slab."""
+    nd = len(shape)
+    st = [1] * nd
+    if nd >= 2:
+        st[nd - 2] = int(P)
+        for k in range(nd - 3, -1, -1):
+            st[k] = st[k + 1] * int(shape[k + 1])
+    return st
+
+
 def swap_perm(ndim, split, kaxes, vaxes):
     """Net permutation and split of BoltArraySpark.swap (array.py:716-763).
 

@@ -101,9 +101,11 @@ class Values(Shapes):
 
 def _relabel(b, newshape, split):
     """``b``'s records under ``newshape`` (same C order).  A row-padded array
-    (one GPU) whose last axis keeps its length keeps its padded rows."""
+    whose last axis keeps its length keeps its padded rows (across GPUs only
+    while the slabs stay put)."""
     d = b.__dict__
-    if "_pbuf" in d and len(newshape) >= 2 and newshape[-1] == b.shape[-1]:
+    if "_pbuf" in d and len(newshape) >= 2 and newshape[-1] == b.shape[-1] and \
+            (b.context.world_size == 1 or newshape[0] == b.shape[0]):
         return b._derive_padded(d["_pbuf"], d["_pitch"], newshape, split)
     return b._like(_reslab(b, newshape), newshape, split)
 

@@ -75,3 +75,74 @@ def test_dist_fuzz_gpu_kernels_one_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _run(2, "cuda:0")
+
+
+def _padded_worker(rank, world, port, errq):
+    """The four seeded suites on padded inputs across ranks (round 6): every
+    array starts as a padded transposition result (tests/test_row_pitch.py's
+    padded_inputs), with the pitch thresholds lowered so small arrays pad, so
+    the exchanges read and write padded slabs."""
+    import sys
+    import numpy as np
+    import torch.distributed as dist
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import bolt_amd
+        import bolt_amd.mi355x.array as A
+        from bolt_amd import MI355XContext
+        import cpu_backend
+        cpu_backend.install()
+        A._PITCH_MIN_ROW, A._PITCH_LINE, A._PITCH_ALIGN, A._PITCH_PAD_DIV = 1, 16, 64, 0
+        A._PITCH_PLANS.clear()
+        orig = bolt_amd.array
+
+        def array(x, context=None, axis=(0,), **kw):
+            x = np.asarray(x)
+            if x.ndim < 2 or context is None or kw:
+                return orig(x, context, axis=axis, **kw)
+            y = np.ascontiguousarray(np.moveaxis(x, -1, 0))
+            return orig(y, context, axis=axis).transpose(*(tuple(range(1, x.ndim)) + (0,)))
+        bolt_amd.array = array
+        ctx = MI355XContext(device="cpu")
+        from test_fuzz_oracle import check_case
+        from test_api_fuzz import test_api_fuzz
+        from test_getitem_fuzz import test_getitem_fuzz
+        from test_chunk_fuzz import test_chunk_fuzz
+        for seed in range(0, 60, 3):
+            for name, f in (("oracle", check_case), ("api", test_api_fuzz), ("getitem", test_getitem_fuzz),
+                            ("chunk", test_chunk_fuzz)):
+                try:
+                    f(ctx, seed)
+                except pytest.skip.Exception:
+                    continue  # a case the suite itself skips (on every rank alike)
+                except Exception:
+                    raise AssertionError("%s seed %d failed" % (name, seed))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_fuzz_padded_gloo(world):
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_padded_worker, args=(r, world, port, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=400)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
+    assert all(p.exitcode == 0 for p in procs)

@@ -364,3 +364,97 @@ def test_gpu_padded_toarray_windows(gpu_ctx, monkeypatch):
     got = s.toarray()
     assert _padded(s) and "_data" not in s.__dict__
     assert got.shape == (256, 512, 500) and got.tobytes() == np.ascontiguousarray(x.transpose(1, 2, 0)).tobytes()
+
+
+def _padded_ranks_body(rank, world):
+    """Padded rows across ranks (round 6): the exchange's unpack writes the
+    swap result at the same pitch rule as one GPU, and every consumer reads it
+    or compacts it, on every rank."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here)]
+    import cpu_backend
+    from bolt_amd import MI355XContext
+    cpu_backend.install()
+    A._PITCH_MIN_ROW, A._PITCH_LINE, A._PITCH_ALIGN, A._PITCH_PAD_DIV = 1, 16, 64, 0
+    A._PITCH_PLANS.clear()
+    ctx = MI355XContext(device="cpu")
+    assert ctx.world_size == world
+    for case, (shape, kax, vax, dtype) in enumerate(CASES):
+        x = _data(shape, dtype, 300 + case)
+        axis = tuple(range(len(kax)))
+        s = bolt.array(x, ctx, axis=axis).swap(kax, vax)
+        assert _padded(s), (rank, case)
+        A.ROW_PITCH = False
+        d = bolt.array(x, ctx, axis=axis).swap(kax, vax)
+        A.ROW_PITCH = True
+        assert not _padded(d)
+        want = d.toarray()
+        last = s.ndim - 1
+        for name in ("mean", "var", "std"):
+            got, ref = np.asarray(getattr(s, name)(axis=last)), np.asarray(getattr(d, name)(axis=last))
+            assert got.shape == ref.shape and got.tobytes() == ref.tobytes(), (rank, case, name)
+        assert _padded(s), "last-axis statistics read the padded slab in place"
+        got = s.toarray()
+        assert _padded(s) and "_data" not in s.__dict__, "toarray compacts window by window"
+        assert got.tobytes() == want.tobytes(), (rank, case)
+        # a padded source across GPUs: the exchange's pack reads it in place
+        back = (tuple(range(len(vax))), tuple(range(len(kax))))
+        t = s.swap(*back)
+        assert _padded(s) and t.toarray().tobytes() == d.swap(*back).toarray().tobytes(), (rank, case)
+        for name, f in _consumers(kax, vax):
+            s2 = bolt.array(x, ctx, axis=axis).swap(kax, vax)
+            g = np.asarray(f(s2))
+            A.ROW_PITCH = False
+            w = np.asarray(f(bolt.array(x, ctx, axis=axis).swap(kax, vax)))
+            A.ROW_PITCH = True
+            assert g.shape == w.shape and g.dtype == w.dtype and g.tobytes() == w.tobytes(), (rank, case, name)
+    # the egress windows: whole rows, several of them, ragged slabs
+    from bolt_amd.mi355x import dist as bdist
+    bdist.EGRESS_WINDOW = 100
+    x = _data((13, 5, 7), np.float32, 9)
+    s = bolt.array(x, ctx).swap((0,), (0, 1))
+    assert _padded(s) and s.toarray().tobytes() == np.ascontiguousarray(x.transpose(1, 2, 0)).tobytes()
+    bdist.EGRESS_WINDOW = None
+
+
+def _padded_ranks_worker(rank, world, port, errq):
+    import traceback
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        _padded_ranks_body(rank, world)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        errq.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_padded_rows_across_ranks_gloo(world):
+    """World 2 / 3 over gloo (CPU executor): both ranks hold padded rows after
+    the swap, statistics and toarray exact, toarray without a dense copy."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    procs = [ctx.Process(target=_padded_ranks_worker, args=(r, world, port, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
+    assert all(p.exitcode == 0 for p in procs)
