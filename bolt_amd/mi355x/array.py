@@ -188,6 +188,21 @@ def _pitch_fits(pp, es, device):
 _padded_strides = padded_strides
 
 
+@functools.lru_cache(maxsize=1024)
+def _aligned_vshape_of(shape, split, axis):
+    """BoltArrayMI355X._aligned_vshape for (shape, split, axes)."""
+    tokeys = [a - split for a in axis if a >= split]
+    tovalues = [a for a in range(split) if a not in axis]
+    if not (tokeys or tovalues):
+        return None
+    ref = swap_shape(shape, split, tovalues, tokeys)
+    if ref is None:
+        return None
+    vs = ref[0][ref[1]:]
+    kept = tuple(d for i, d in enumerate(shape) if i not in set(axis))
+    return None if vs == kept else vs
+
+
 _REDUCE_PLANS = {}  # (local shape, axes, stat, dtype, world) -> device reduction plan
 _STAT_AXES = {}  # (shape, split, axis as given) -> (validated axes, records after _align, record shape | None)
 
@@ -1268,16 +1283,10 @@ class BoltArrayMI355X(BoltArray):
         """The record shape after the reference's _align(axis) (array.py:85-115)
         when its swap squeezes a unit axis (plan.swap_shape), else None: the
         kept axes' extents in ascending order."""
-        tokeys = [a - self._split for a in axis if a >= self._split]
-        tovalues = [a for a in range(self._split) if a not in axis]
-        if not (tokeys or tovalues):
-            return None
-        ref = swap_shape(self._shape, self._split, tovalues, tokeys)
-        if ref is None:
-            return None
-        vs = ref[0][ref[1]:]
-        kept = tuple(d for i, d in enumerate(self._shape) if i not in set(int(a) for a in axis))
-        return None if vs == kept else vs
+        try:
+            return _aligned_vshape_of(self._shape, self._split, tuple(int(a) for a in axis))
+        except TypeError:
+            return _aligned_vshape_of.__wrapped__(self._shape, self._split, tuple(axis))
 
     def _nrecords(self, axis):
         """Records the reduction sees after _align: the product of the reduced extents."""
