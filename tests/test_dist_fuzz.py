@@ -77,7 +77,7 @@ def test_dist_fuzz_gpu_kernels_one_device():
     _run(2, "cuda:0")
 
 
-def _padded_worker(rank, world, port, errq):
+def _padded_worker(rank, world, port, errq, device="cpu"):
     """The four seeded suites on padded inputs across ranks (round 6): every
     array starts as a padded transposition result (tests/test_row_pitch.py's
     padded_inputs), with the pitch thresholds lowered so small arrays pad, so
@@ -95,7 +95,10 @@ def _padded_worker(rank, world, port, errq):
         import bolt_amd.mi355x.array as A
         from bolt_amd import MI355XContext
         import cpu_backend
-        cpu_backend.install()
+        if device == "cpu":
+            cpu_backend.install()
+        else:
+            cpu_backend.install_host_staged_gpu()
         A._PITCH_MIN_ROW, A._PITCH_LINE, A._PITCH_ALIGN, A._PITCH_PAD_DIV = 1, 16, 64, 0
         A._PITCH_PLANS.clear()
         orig = bolt_amd.array
@@ -107,7 +110,7 @@ def _padded_worker(rank, world, port, errq):
             y = np.ascontiguousarray(np.moveaxis(x, -1, 0))
             return orig(y, context, axis=axis).transpose(*(tuple(range(1, x.ndim)) + (0,)))
         bolt_amd.array = array
-        ctx = MI355XContext(device="cpu")
+        ctx = MI355XContext(device=device)
         from test_fuzz_oracle import check_case
         from test_api_fuzz import test_api_fuzz
         from test_getitem_fuzz import test_getitem_fuzz
@@ -128,12 +131,11 @@ def _padded_worker(rank, world, port, errq):
         raise
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_dist_fuzz_padded_gloo(world):
+def _run_padded(world, device):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_padded_worker, args=(r, world, port, errq)) for r in range(world)]
+    procs = [ctx.Process(target=_padded_worker, args=(r, world, port, errq, device)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -146,3 +148,18 @@ def test_dist_fuzz_padded_gloo(world):
             p.kill()
     assert not errs, "\n".join("rank %d:\n%s" % e for e in errs)
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_fuzz_padded_gloo(world):
+    _run_padded(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_dist_fuzz_padded_gpu_kernels_one_device():
+    """The same on the HIP kernels: 2 ranks sharing cuda:0, the exchanges
+    staged through the host (RCCL refuses two ranks on one GPU)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _run_padded(2, "cuda:0")
