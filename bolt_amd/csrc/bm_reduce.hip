@@ -42,9 +42,15 @@ constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: gr
 constexpr int kColsUnroll = 8;
 // split R over blocks below this many column tiles; column vectors per block
 // at most (the rest of the 256 lanes are row phases); the narrowest tile taken
-// to reach kColsBlocks before chunking R (profiles/r03zb_ab_tcv.log, r03zc_ab_tcv_rule.log)
+// to reach kColsBlocks before chunking R (profiles/r03zb_ab_tcv.log, r03zc_ab_tcv_rule.log).
+// Round 6: 64-vector tiles (four row phases per block) for every shape, not
+// only the few-tile ones: the 64 GiB target's mean / std over axis 0
+// +0.8..+1.8% on two placements, 128-vector tiles +0.7..+1.7%, C2 / C4
+// columns +-0.3% (profiles/r06j_ab_cols_tiles.log, r06k_ab_cols_tiles.log; the
+// column kernels had 4x the rows kernel's DRAM read-credit stalls per byte,
+// r06i_cols_vs_rows_counters.md); 32 B per lane lost 6-12%
 constexpr int64_t kColsBlocks = 2048;
-constexpr int64_t kColsTcv = 256;
+constexpr int64_t kColsTcv = 64;
 constexpr int64_t kColsTcvMin = 64;
 // 16-B vectors in flight per lane in the rows kernel: 2 beats 4 by 4%, 8 by 25%
 // (profiles/r01_ab1.log; 3: equal, 4: -5% again on padded rows, r05z_rows_unroll.txt)
