@@ -38,7 +38,9 @@ constexpr int64_t kMaxBlocks = 0xffffffffLL / kThreads;  // HIP launch limit: gr
 // Shipped parameters (the A/B runs that chose them are cited; the rejected
 // values live in git history and tools/microbench/):
 // rows in flight per lane in the column reductions: 8 over 4 +1.2-1.4% on the
-// 64 GiB target mean / std and C2-shape columns, 2 -4-8% (profiles/r02_ab_cols.log)
+// 64 GiB target mean / std and C2-shape columns, 2 -4-8% (profiles/r02_ab_cols.log);
+// on round 6's 64-vector tiles 16 is within +0.2..+1.4% of 8 (two placements,
+// profiles/r06l_ab_cols_unroll.log): 8 stays (half the load registers)
 constexpr int kColsUnroll = 8;
 // split R over blocks below this many column tiles; column vectors per block
 // at most (the rest of the 256 lanes are row phases); the narrowest tile taken
