@@ -17,8 +17,6 @@ scatter for trailing keys, a masked record gather for values_to_keys), and
 otherwise unpack -> permute (RCCL all-to-all if the sharded axis moves) ->
 pack.
 """
-import os
-
 import numpy as np
 
 from bolt_amd.mi355x.context import local_shape
@@ -30,16 +28,29 @@ from bolt_amd.mi355x.plan import (ChunkGeometry, getplan, check_plan, getnumber,
 RECORD_MAP_MAX_BYTES = 65536  # a source record staged whole in LDS (bm_record_gather)
 
 
+# Which of the equivalent chunk paths run.  Every path gives the same bytes;
+# tests/test_chunk_paths.py flips these to compare them with each other:
+#   fused_rechunk  keys_to_values / values_to_keys packed -> packed in one pass
+#                  (False: unpack -> permute -> pack)
+#   scatter        "on": unchunk / keys_to_values / values_to_keys of small
+#                  records as one record scatter where its writes are whole
+#                  runs; "off": strided copies / record gather; "force": the
+#                  scatter also where its writes would be piecewise
+#   runs           keys_to_values whose records are a few long runs as
+#                  bm_record_runs (False: the map scatter)
+#   record_map     small records packed by one record-map gather (False: one
+#                  strided copy per chunk run)
+PATHS = {"fused_rechunk": True, "scatter": "on", "runs": True, "record_map": True}
+
+
 def _fused_rechunk():
-    """keys_to_values / values_to_keys packed -> packed (A/B knob BOLT_AMD_FUSED_RECHUNK=0)."""
-    return os.environ.get("BOLT_AMD_FUSED_RECHUNK", "1") != "0"
+    return bool(PATHS["fused_rechunk"])
 
 
 def _use_scatter():
     """unchunk / keys_to_values / values_to_keys of small records as one
-    record scatter (bm_record_scatter; A/B knob BOLT_AMD_SCATTER=0, tests
-    BOLT_AMD_SCATTER=force: also where its writes would be piecewise)."""
-    return os.environ.get("BOLT_AMD_SCATTER", "1") != "0"
+    record scatter (bm_record_scatter)."""
+    return PATHS["scatter"] != "off"
 
 
 _SCATTER_PLANS = {}
@@ -50,12 +61,12 @@ def _scatter_plan(key, build, src_rec, gstride, es):
     a record scatter or would write lines piecewise (plan.scatter_runs_ok);
     built once per key (geometry, move, element size)."""
     from bolt_amd.mi355x.plan import scatter_vec, scatter_runs_ok
-    key = key + (os.environ.get("BOLT_AMD_SCATTER"),)
+    key = key + (PATHS["scatter"],)
     if key in _SCATTER_PLANS:
         return _SCATTER_PLANS[key]
     maps = build()
     plan = None
-    force = os.environ.get("BOLT_AMD_SCATTER") == "force"
+    force = PATHS["scatter"] == "force"
     if maps is not None and (force or scatter_runs_ok(maps[0], maps[1], es)):
         map_a, map_b = maps
         plan = (map_a, map_b, scatter_vec(map_a, map_b, src_rec, gstride, es))
@@ -66,9 +77,8 @@ def _scatter_plan(key, build, src_rec, gstride, es):
 
 
 def _use_runs():
-    """keys_to_values whose records are a few long runs as bm_record_runs (A/B
-    knob BOLT_AMD_RUNS=0: the map scatter)."""
-    return os.environ.get("BOLT_AMD_RUNS", "1") != "0"
+    """keys_to_values whose records are a few long runs as bm_record_runs."""
+    return bool(PATHS["runs"])
 
 
 _RUNS_PLANS = {}
@@ -86,7 +96,7 @@ def _runs_plan(key, plan, src_rec, gstride, es):
 
 def _use_record_map(src_rec, es):
     """Small records: one record-map gather instead of a strided copy per chunk run."""
-    if os.environ.get("BOLT_AMD_RECORD_MAP", "1") == "0":  # A/B knob
+    if not PATHS["record_map"]:
         return False
     return es in (1, 2, 4, 8) and 0 < src_rec * es <= RECORD_MAP_MAX_BYTES
 

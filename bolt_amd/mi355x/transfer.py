@@ -6,7 +6,7 @@ path is PCIe (63 GB/s spec, MI355X_MICROARCH.md).
 
 Ingest: the runtime's own pageable copy reaches 56 GB/s on the box, ahead of
 staging through page-locked chunks (54 GB/s at 8 copy threads,
-profiles/r01_transfer_*.log), so it is the default (BOLT_AMD_H2D=staged
+profiles/r01_transfer_*.log), so it is the default (H2D_DIRECT = False
 selects the staged path).  Egress: a pageable D2H bounces through the
 driver's staging at 6-8 GB/s, so large results are staged through two
 page-locked chunks from torch's caching host allocator -- the host memcpy of
@@ -14,19 +14,18 @@ chunk i (split over 8 threads; numpy releases the GIL) overlaps the DMA of
 chunk i+1 -- 17-18 GB/s, bound by first-touch page faults of the fresh numpy
 result.  Small transfers take one pinned buffer and return a view of it.
 """
-import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-CHUNK = int(os.environ.get("BOLT_AMD_COPY_CHUNK_MB", "64")) << 20   # bytes per staging chunk
+CHUNK = 64 << 20          # bytes per staging chunk
 SMALL = 8 << 20           # below this: one pinned buffer, no pipeline
-THREADS = int(os.environ.get("BOLT_AMD_COPY_THREADS", "8"))        # host memcpy threads per chunk
-H2D_DIRECT = os.environ.get("BOLT_AMD_H2D", "direct") == "direct"  # the runtime's pageable copy
+THREADS = 8               # host memcpy threads per chunk
+H2D_DIRECT = True         # ingest through the runtime's pageable copy (False: staged)
 
 # statistics results up to SMALL bytes are stored by the reduction kernel
 # straight into a page-locked host buffer (no D2H copy launch)
-ZERO_COPY = os.environ.get("BOLT_AMD_ZERO_COPY", "1") != "0"
+ZERO_COPY = True
 
 _POOL = None
 

@@ -55,7 +55,7 @@ def test_record_map_matches_strided_copies(bctx, case, monkeypatch):
     b = bolt.array(x, bctx, axis=tuple(range(split)))
     packs = {}
     for use_map in (True, False):
-        monkeypatch.setenv("BOLT_AMD_RECORD_MAP", "1" if use_map else "0")
+        monkeypatch.setitem(chunk_mod.PATHS, "record_map", use_map)
         c = b.chunk(size, padding=padding)
         packs[use_map] = c
         assert np.asarray(c.unchunk().toarray()).tobytes() == x.tobytes()
@@ -109,7 +109,7 @@ def test_fused_rechunk_matches_dense_path(bctx, case, dtype, monkeypatch):
     c = b.chunk(size, padding=padding)
     res = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("BOLT_AMD_FUSED_RECHUNK", fused)
+        monkeypatch.setitem(chunk_mod.PATHS, "fused_rechunk", fused == "1")
         res[fused] = c.keys_to_values(axes, size=ksize) if op == "k2v" else c.values_to_keys(axes)
     f, d = res["1"], res["0"]
     assert f.shape == d.shape and f.split == d.split
@@ -187,7 +187,7 @@ def test_record_scatter_paths_match(bctx, monkeypatch, shape, split, dtype, plan
     x = rng.integers(0, 200, size=shape).astype(dtype)
     out = {}
     for mode in ("0", "force"):
-        monkeypatch.setenv("BOLT_AMD_SCATTER", mode)
+        monkeypatch.setitem(chunk_mod.PATHS, "scatter", "off" if mode == "0" else mode)
         c = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad)
         k2v = c.keys_to_values((split - 1,))
         v2k = c.values_to_keys((0,))
@@ -258,8 +258,8 @@ def test_record_runs_path_matches(bctx, monkeypatch, shape, split, dtype, plan, 
     monkeypatch.setattr(be, "record_runs", lambda *a, **k: (calls.append(a[4:8]), orig(*a, **k))[1])
     out = {}
     for runs, scatter in (("1", "1"), ("0", "1"), ("0", "0")):
-        monkeypatch.setenv("BOLT_AMD_RUNS", runs)
-        monkeypatch.setenv("BOLT_AMD_SCATTER", scatter)
+        monkeypatch.setitem(chunk_mod.PATHS, "runs", runs == "1")
+        monkeypatch.setitem(chunk_mod.PATHS, "scatter", "on" if scatter == "1" else "off")
         c = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad)
         k = c.keys_to_values((split - 1,))
         out[runs + scatter] = (k._packed.cpu().numpy().tobytes(), k.unchunk().toarray().tobytes())
@@ -329,8 +329,8 @@ def test_record_runs_fuzz(bctx, monkeypatch, case):
     x = rng.integers(0, 250, size=shape).astype(dtype)
     out = {}
     for runs, scatter in (("1", "1"), ("0", "0")):
-        monkeypatch.setenv("BOLT_AMD_RUNS", runs)
-        monkeypatch.setenv("BOLT_AMD_SCATTER", scatter)
+        monkeypatch.setitem(chunk_mod.PATHS, "runs", runs == "1")
+        monkeypatch.setitem(chunk_mod.PATHS, "scatter", "on" if scatter == "1" else "off")
         c = bolt.array(x, bctx, axis=tuple(range(split))).chunk(plan, padding=pad)
         k = c.keys_to_values((split - 1,))
         out[runs] = (k._packed.cpu().numpy().tobytes(), k.unchunk().toarray().tobytes(), k.plan.tolist(),

@@ -67,7 +67,8 @@ def main():
             del v
         del b, c, u
         torch.cuda.empty_cache()
-    res["record_map"] = os.environ.get("BOLT_AMD_RECORD_MAP", "1")
+    from bolt_amd.mi355x.chunk import PATHS
+    res["paths"] = dict(PATHS)
     print(json.dumps(res, indent=1))
 
 

@@ -1,5 +1,5 @@
 """Wall time of C2's statistics with the result stored by the kernel into
-page-locked host memory (BOLT_AMD_ZERO_COPY, transfer.host_result) vs a
+page-locked host memory (transfer.ZERO_COPY, transfer.host_result) vs a
 device buffer + D2H copy.  Interleaved rounds, median per call.
 
     python tools/zero_copy_probe.py
