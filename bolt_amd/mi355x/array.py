@@ -70,6 +70,7 @@ def _tree(func, recs):
         recs = nxt
     return recs[0]
 # reductions whose result keeps the input dtype (numpy's same-dtype ufunc rule)
+_MOMENTS = (_lib.STAT_MEAN, _lib.STAT_VAR, _lib.STAT_STD)
 _KEEP_DTYPE = (_lib.STAT_SUM, _lib.STAT_MAX, _lib.STAT_MIN, _lib.STAT_PROD, _lib.STAT_BAND,
                _lib.STAT_BOR, _lib.STAT_BXOR, _lib.STAT_FMAX, _lib.STAT_FMIN)
 
@@ -1081,6 +1082,10 @@ class BoltArrayMI355X(BoltArray):
                 be.reduce(stat, pbuf, code, O, R, Ip, out, ocode)
                 full = to_host(out, out_dtype, (O, I // Rl, P))
             return np.ascontiguousarray(full[:, :, :Rl]).reshape(out_shape), out_dtype
+        if pbuf is not None and perm is None and O == 1 and I == 1 and R == nloc and nloc \
+                and ctx.world_size == 1 and len(lshape) >= 2 and stat in _MOMENTS \
+                and self._dtype.kind == "f" and self._dtype.itemsize >= 4:
+            return self._padded_all_moments(pbuf, stat, code, out_dtype, out_shape), out_dtype
         be = self._backend
         dev = self._device
         es = self._dtype.itemsize
@@ -1138,6 +1143,32 @@ class BoltArrayMI355X(BoltArray):
         out = _empty(nout * out_dtype.itemsize, dev)
         be.reduce_combine(stat, code, states, counts, nout, out, ocode)
         return to_host(out, out_dtype, out_shape), out_dtype
+
+    def _padded_all_moments(self, pbuf, stat, code, out_dtype, out_shape):
+        """mean / var / std over every axis of a row-padded float array, read in
+        place: the padded rows are one (rows, pitch) matrix whose columns get a
+        float64 mean (and M2 for var / std) state each over all rows
+        (bm_reduce_state, the pad columns' states dropped); the row-length states, all of the same count,
+        merge on the host -- the StatCounter merge of statcounter.py:67-99 for
+        equal counts: mean = mean of the column means, M2 = sum of the column
+        M2 + rows * sum of squared deviations of the column means.  No dense
+        copy of the array is made; the summation order differs from the dense
+        layout's (results within 1e-12 relative in float64, rounded once)."""
+        be = backend_for(pbuf.device)
+        Rl, P = self._local_shape[-1], self._pitch
+        nrows = int(np.prod(self._local_shape[:-1], dtype=np.int64))
+        state = _empty(be.state_bytes(stat, code, P), pbuf.device)
+        be.reduce_state(stat, pbuf, code, 1, nrows, P, state)
+        planes = to_host(state, np.float64, (-1, P))   # mean [, M2] (bm_reduce_state)
+        means = planes[0, :Rl]
+        mean = means.mean()
+        if stat == _lib.STAT_MEAN:
+            v = mean
+        else:
+            v = (planes[1, :Rl].sum() + nrows * np.square(means - mean).sum()) / (nrows * Rl)
+            if stat == _lib.STAT_STD:
+                v = np.sqrt(v)
+        return np.asarray(v, dtype=np.float64).astype(out_dtype).reshape(out_shape)
 
     def _stat(self, axis=None, func=None, name=None, keepdims=False):
         """Statistic over ``axis`` (array.py:284-334); results are host arrays / scalars."""

@@ -212,6 +212,20 @@ def test_stats_full_size_c2(gpu_ctx):
     assert np.all(np.abs(v - vref) <= 1e-6 * vref + np.spacing(np.float32(vref)))
     tot = b.sum()
     assert abs(float(tot) - float(x.sum())) <= 1e-6 * abs(float(x.sum()))
+    # every axis of the padded result: per-column states over the padded rows
+    # merged on the host, no dense copy; against the float64 truth and the
+    # dense layout's answer (rtol 1e-6 + the float32 rounding)
+    n = x.numel()
+    t_mean = float(x.sum()) / n
+    t_var = float(((x - t_mean) ** 2).sum()) / n
+    d = b.swap((0,), (0, 1))
+    d._compact()
+    for name, truth in (("mean", t_mean), ("var", t_var), ("std", t_var ** 0.5)):
+        got = getattr(s, name)()
+        assert "_pbuf" in s.__dict__ and "_data" not in s.__dict__, name
+        bar = 1e-6 * abs(truth) + float(np.spacing(np.float32(abs(truth))))
+        assert np.float32(got).dtype == np.float32 and abs(float(got) - truth) <= bar, (name, got, truth)
+        assert abs(float(got) - float(getattr(d, name)())) <= bar, name
 
 
 def test_stats_full_size_c4_var(gpu_ctx):

@@ -111,8 +111,15 @@ def test_padded_statistics(bctx, small_pitch, case):
     m0 = np.asarray(s.max(axis=0))
     assert m0.tobytes() == np.maximum.reduce(want, axis=0).tobytes()
     assert _padded(s)
-    # over every axis: compacts, then the dense path answers
-    assert np.allclose(s.mean(), want.astype(np.float64).mean(), rtol=1e-5, atol=1e-6)
+    # over every axis: moments of float rows are read in place (per-column states
+    # over the padded rows, merged on the host); anything else compacts first
+    w64 = want.astype(np.float64)
+    for name in ("mean", "var", "std"):
+        got = getattr(s, name)()
+        assert np.allclose(got, getattr(w64, name)(), rtol=1e-5, atol=1e-6), name
+    if np.dtype(dtype).kind == "f":
+        assert _padded(s) and "_data" not in s.__dict__
+    s.sum()
     assert not _padded(s)
     assert s.toarray().tobytes() == want.tobytes()
 
