@@ -41,3 +41,21 @@ def test_random_chains_with_unit_axes_match_the_reference(tmp_path):
                        env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=900)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "seeds 0..1499: 0 failed" in out, out[-4000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "bolt", "spark")), reason="reference not present")
+@pytest.mark.parametrize("seed,min_extent", [(15168, "2"), (31731, "1")])
+def test_advanced_index_after_a_shuffle(tmp_path, seed, min_extent):
+    """The two chains of the round-6 soak (seeds 12,000-40,000) where the
+    reference's answer differed: a list index on every axis of an array whose
+    RDD a transpose had shuffled.  The reference numbers the selected records
+    in the RDD's current order (array.py:552), the partitioner's; bolt_amd in
+    key order, the reference's answer on the same array in key order
+    (docs/HISTORY.md §4 item 9), which the fuzz compares against."""
+    env = dict(os.environ)
+    env["PYTHONDONTWRITEBYTECODE"] = "1"
+    env["BOLT_AMD_DIFF_MIN_EXTENT"] = min_extent
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "reference_diff_fuzz.py"), str(seed), str(seed + 1)],
+                       env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "seeds %d..%d: 0 failed" % (seed, seed) in out and "'getitem': 1" in out, out[-4000:]

@@ -17,7 +17,9 @@ around: length-1 axes are not generated, records are compared in key order,
 paddings that trigger removepad's over-trim are not drawn, an array the
 reference builds but cannot collect must raise ValueError here, a transpose
 of an all-key array (which the reference cannot do) must be numpy's, and
-filter is compared in key order (the reference's sort=True).
+filter is compared in key order (the reference's sort=True), and so is a
+list index on every axis of an array a shuffle left out of key order (the
+reference applied to the same array in key order).
 
     PYTHONDONTWRITEBYTECODE=1 python tools/reference_diff_fuzz.py 0 2000
     BOLT_AMD_DIFF_PADDED=1 ... (the same with padded rows for small arrays)
@@ -218,7 +220,16 @@ def one_case(seed, sc, ctx):
             index = _index(rng, r.shape, split)
             if index is None:
                 continue
-            rv, ov = run_both(lambda: r[index], lambda: o[index])
+            rr = r
+            if not getattr(r, "_ordered", True) and isinstance(index, tuple) and \
+                    all(isinstance(i, list) for i in index):
+                # advanced indexing numbers the selected records in the RDD's
+                # current order (array.py:552 zipWithIndex), which after a
+                # shuffle is the partitioner's, not key order (docs/HISTORY.md
+                # §4 item 9): compared with the reference on the same array in
+                # key order
+                rr = ref_bolt.array(ref_array(r), sc, axis=tuple(range(r.split)))
+            rv, ov = run_both(lambda: rr[index], lambda: o[index])
             if ov is None:
                 continue
             if hasattr(rv, "_rdd"):
