@@ -129,6 +129,7 @@ class HipBackend(object):
         self.lib = _lib.load()
         self._maps = {}  # (device, geometry key) -> resident int32 record map
         self._args = {}  # (shape, perm) -> ctypes arguments of bm_permute
+        self._cargs = {}  # (shape, strides, strides) -> ctypes arrays of bm_copy_strided
         self._ws = {}    # reduction -> workspace bytes
 
     # Pointer and stream arguments go to ctypes as plain ints (the argtypes
@@ -153,10 +154,19 @@ class HipBackend(object):
         nd = len(shape)
         if nd == 0:
             shape, sstrides, dstrides, nd = [1], [1], [1], 1
-        _lib.check(self.lib.bm_copy_strided(self._ptr(src, src_off), self._ptr(dst, dst_off), nd,
-                                            _lib.i64_array(shape), _lib.i64_array(sstrides),
-                                            _lib.i64_array(dstrides), int(es), self._stream(src)),
-                   "bm_copy_strided")
+        # the swap's launch path repeats one (shape, strides) per call: its
+        # three int64 arrays are built once (~5 us of ctypes per call)
+        key = (tuple(shape), tuple(sstrides), tuple(dstrides))
+        args = self._cargs.get(key)
+        if args is None:
+            args = (_lib.i64_array(shape), _lib.i64_array(sstrides), _lib.i64_array(dstrides))
+            if len(self._cargs) > 4096:
+                self._cargs.clear()
+            self._cargs[key] = args
+        rc = self.lib.bm_copy_strided(self._ptr(src, src_off), self._ptr(dst, dst_off), nd,
+                                      args[0], args[1], args[2], int(es), self._stream(src))
+        if rc:
+            _lib.check(rc, "bm_copy_strided")
 
     def permute(self, src, shape, perm, es, dst):
         key = (tuple(shape), tuple(perm))
