@@ -366,6 +366,12 @@ OPS = {
     "c4_var_full": lambda: Reduce(1, 1, 10000, 1024 * 1024, np.uint16, np.float64),
     "u16_var_rows": lambda: Reduce(1, 1024 * 1024, 2000, 1, np.uint16, np.float64),
     "c5_T": lambda: Permute((64, 64, 64, 64, 64), (4, 3, 2, 1, 0), np.float64),
+    # statistics over every axis: a rows pass into chunk partials + the block combine
+    "c1_mean_all": lambda: Reduce(0, 1, 100 * 64 * 64, 1, np.float64, np.float64),
+    "c1_var_all": lambda: Reduce(1, 1, 100 * 64 * 64, 1, np.float64, np.float64),
+    "c1_sum_all": lambda: Reduce(3, 1, 100 * 64 * 64, 1, np.float64, np.float64),
+    "c2_mean_all": lambda: Reduce(0, 1, 2000 * 512 * 512, 1, np.float32, np.float32),
+    "c2_var_all": lambda: Reduce(1, 1, 2000 * 512 * 512, 1, np.float32, np.float32),
     "c5_perm": lambda: Permute((64, 64, 64, 64, 64), (2, 0, 4, 1, 3), np.float64),
 }
 
