@@ -1200,6 +1200,34 @@ class KernelClock(object):
         return len(self.pairs.get(op, ())) / float(steps)
 
 
+def live_copy_gbps(be, dev, nbytes, reps=7):
+    """The box's copy ceiling for the headline kernel's byte count, measured
+    here: the library's contiguous copy (bm_copy_strided -> 16-B rowcopy) of
+    ``nbytes`` into a second buffer, hipEvents on the launch stream, median of
+    ``reps`` after one untimed call.  Algorithmic bytes 2 * nbytes.  None off
+    the GPU.  (Run after the timed region; its buffers are freed.)"""
+    import torch
+    if dev.type != "cuda" or nbytes < (1 << 20):
+        return None
+    n4 = int(nbytes) // 4
+    src = torch.empty(n4 * 4, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(1)
+    ms = []
+    for i in range(reps + 1):
+        e0, e1 = make_event(dev), make_event(dev)
+        e0.record()
+        be.copy_strided(src, 0, dst, 0, [n4], [1], [1], 4)
+        e1.record()
+        e1.synchronize()
+        if i:
+            ms.append(e0.elapsed_time(e1))
+    del src, dst
+    _empty_cache(torch, dev)
+    ms.sort()
+    return 2.0 * n4 * 4 / (ms[len(ms) // 2] / 1e3) / 1e9
+
+
 def _stdout_to_stderr(fn):
     """Run fn with file descriptor 1 pointed at 2: the process group's
     transports print connection chatter on stdout ("[Gloo] Rank 0 is connected
@@ -1592,6 +1620,12 @@ def main():
             else:
                 line["rccl_ranks"] = None
         line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
+        # this box's own copy ceiling for the same bytes (boxes differ by up to
+        # ~25% on the same kernel, profiles/r06zk_pack_expand.log)
+        copy_live = live_copy_gbps(be, dev, ops[0][2] // 2)
+        if copy_live:
+            line["roofline"]["copy_live"] = round(copy_live, 1)
+            line["roofline"]["frac_of_live_copy"] = round(line["roofline"]["achieved"] / copy_live, 4)
         stat_ops = [name for name, _, _ in ops[1:] if name in ("mean", "std", "var")]
         if stat_ops and world == 1:
             # the reduction kernels' own hipEvents, in K more steps (kept out of the
