@@ -14,7 +14,12 @@ buffers, interleaved:
   copy     torch copy_ of the 8.6 GB source into the destination's front
 ms per call, median of 7 rounds x 3 calls; outputs of expand / ident checked.
 
-    python tools/pack_expand_probe.py
+    python tools/pack_expand_probe.py [churn_gib]
+
+churn_gib: first allocate and free that many GiB (torch's caching allocator
+hands them back to the driver), as the bench's earlier configs do before C5
+(the 64 GiB target alone holds 128 GiB), so the C5 buffers land on the pages
+a long process is given.
 """
 import ctypes
 import os
@@ -31,6 +36,15 @@ from bolt_amd.mi355x import _lib, _ops, plan  # noqa: E402
 def main():
     lib = _lib.load()
     dev = torch.device("cuda", 0)
+    churn = float(sys.argv[1]) if len(sys.argv) > 1 else 0.0
+    if churn > 0:
+        blocks = [torch.empty(16 << 30, dtype=torch.uint8, device=dev) for _ in range(int(churn // 16))]
+        for t in blocks:
+            t.fill_(7)
+        torch.cuda.synchronize()
+        del blocks
+        torch.cuda.empty_cache()
+        print("churned %.0f GiB" % churn, flush=True)
     st = torch.cuda.current_stream(dev).cuda_stream
     nrec, src_rec = 64 ** 3, 64 * 64
     geom = plan.ChunkGeometry((64, 64), (16, 16), (2, 2))
