@@ -1622,7 +1622,7 @@ def main():
         line["roofline"]["frac_of_measured_copy"] = round(line["roofline"]["achieved"] / HBM_COPY_GBPS, 4)
         # this box's own copy ceiling for the same bytes (boxes differ by up to
         # ~25% on the same kernel, profiles/r06zk_pack_expand.log)
-        copy_live = live_copy_gbps(be, dev, ops[0][2] // 2)
+        copy_live = live_copy_gbps(be, dev, ops[0][2] // 2) if world == 1 else None
         if copy_live:
             line["roofline"]["copy_live"] = round(copy_live, 1)
             line["roofline"]["frac_of_live_copy"] = round(line["roofline"]["achieved"] / copy_live, 4)
