@@ -45,12 +45,13 @@ def test_random_chains_with_unit_axes_match_the_reference(tmp_path):
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "bolt", "spark")), reason="reference not present")
 @pytest.mark.parametrize("seed,min_extent,op", [(15168, "2", "getitem"), (31731, "1", "getitem"),
+                                                (204533, "1", "getitem"),
                                                 (60771, "1", "ufunc"), (65282, "2", "ufunc")])
 def test_soak_chains_replayed(tmp_path, seed, min_extent, op):
-    """Chains of the round-6 soak (250,000 seeds) where the reference's
+    """Chains of the round-6 soak (710,000 seeds) where the reference's
     answer differed, replayed:
-      getitem  a list index on every axis of an array whose RDD a transpose had
-               shuffled: the reference numbers the selected records in the
+      getitem  a list index on every axis (a plain list on a 1-D array too) of
+               an array whose RDD a transpose had shuffled: the reference numbers the selected records in the
                RDD's current order (array.py:552), the partitioner's; bolt_amd
                in key order, the reference's answer on the same array in key
                order (docs/HISTORY.md §4 item 9), which the fuzz compares to;

@@ -221,8 +221,8 @@ def one_case(seed, sc, ctx):
             if index is None:
                 continue
             rr = r
-            if not getattr(r, "_ordered", True) and isinstance(index, tuple) and \
-                    all(isinstance(i, list) for i in index):
+            if not getattr(r, "_ordered", True) and (isinstance(index, list) or (
+                    isinstance(index, tuple) and all(isinstance(i, list) for i in index))):
                 # advanced indexing numbers the selected records in the RDD's
                 # current order (array.py:552 zipWithIndex), which after a
                 # shuffle is the partitioner's, not key order (docs/HISTORY.md
