@@ -48,7 +48,7 @@ def test_random_chains_with_unit_axes_match_the_reference(tmp_path):
                                                 (204533, "1", "getitem"),
                                                 (60771, "1", "ufunc"), (65282, "2", "ufunc")])
 def test_soak_chains_replayed(tmp_path, seed, min_extent, op):
-    """Chains of the round-6 soak (710,000 seeds) where the reference's
+    """Chains of the round-6 soak (930,000 seeds) where the reference's
     answer differed, replayed:
       getitem  a list index on every axis (a plain list on a 1-D array too) of
                an array whose RDD a transpose had shuffled: the reference numbers the selected records in the
